@@ -1,0 +1,154 @@
+/*
+ * tfhe_aes_gpu.h -- C-ABI of the MI355X-native FHE AES-128 evaluator (drop-in boundary).
+ *
+ * Plain C types only (opaque handles, pointers, sizes, int status codes); no torch/HIP types.
+ * Every entry point names the reference interface it replaces (allanbrondum/tfhe-aes-2 @
+ * 2025-03-07, paths relative to the reference root).  The reference is in-process Rust; these
+ * are the symbols a Rust `extern "C"` shim implementing its traits would bind.
+ *
+ * Conventions
+ *   - LWE ciphertexts are u64 arrays in the tfhe layout [a_0 .. a_{K-1}, b] (K = k*N, big key);
+ *     a byte is 8 ciphertexts MSB-first (src/util.rs:33-42); a block is 16 bytes in block order;
+ *     an expanded key is 44 words x 4 bytes (fhe.rs:16-38, [Word; 44]).
+ *   - Errors are status codes instead of the reference's panics; tae_last_error() gives the
+ *     message of the calling thread's last failure.
+ *   - A context is bound to one GPU and internally serialised: safe to share across host
+ *     threads (the reference's FheContext is Send + Sync).
+ *   - There is no CPU fallback: without a usable GPU, context creation fails with TAE_E_NODEV.
+ */
+#ifndef TFHE_AES_GPU_H
+#define TFHE_AES_GPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes (the reference panics: "NoiseTooBig", "noise components not independent") */
+#define TAE_OK 0
+#define TAE_E_NOISE 1     /* MaxNoiseLevel::validate -> NoiseTooBig (shortint_woppbs_1bit.rs:74-76) */
+#define TAE_E_INDEP 2     /* "noise components not independent" (shortint_woppbs_1bit.rs:64-70) */
+#define TAE_E_PARAM 3     /* invalid parameter / unsupported shape */
+#define TAE_E_HIP 4       /* HIP runtime failure */
+#define TAE_E_ARG 5       /* invalid argument (null pointer, size mismatch) */
+#define TAE_E_NODEV 6     /* no GPU available: the product path has no CPU fallback */
+
+/* parameter sets: src/tfhe/shortint_woppbs_1bit/parameters.rs */
+#define TAE_PARAMS_SQRD_LVL_1 0   /* :29-61  */
+#define TAE_PARAMS_SQRD_LVL_4 1   /* :77-109 */
+#define TAE_PARAMS_SQRD_LVL_64 2  /* :125-157, default (bin/main.rs:82-83) */
+#define TAE_PARAMS_SQRD_LVL_256 3 /* :173-205 */
+
+/* memory kinds for the raw-array entry points */
+#define TAE_MEM_HOST 0
+#define TAE_MEM_DEVICE 1
+
+typedef struct tae_client_key tae_client_key; /* shortint_woppbs_1bit::ClientKey (:189-195) */
+typedef struct tae_context tae_context;       /* shortint_woppbs_1bit::FheContext (:165-172) */
+typedef struct tae_bit tae_bit;               /* shortint_woppbs_1bit::BitCt (:26-32) */
+typedef struct tae_lut tae_lut;               /* tfhe::shortint::wopbs::WopbsLUTBase */
+
+typedef struct {
+    int n, k, N, pbs_l, pbs_b, ks_l, ks_b, cbs_l, cbs_b, pfks_l, pfks_b;
+    double lwe_std, glwe_std, pfks_std;
+    uint64_t max_noise_sq;
+} tae_params;
+
+const char *tae_last_error(void);
+const char *tae_version(void);
+int tae_device_count(int *count);
+int tae_get_params(int param_set, tae_params *out); /* parameters::params_sqrd_lvl_* */
+
+/* ---- keys (FheContext::generate_keys_with_params, shortint_woppbs_1bit.rs:245-268) ----------
+ * Client key generation on the host from a 32-byte seed (ChaCha20 streams, DESIGN.md keygen
+ * spec), server keys uploaded to `device` and the bootstrapping key converted to the Fourier
+ * domain there.  generate_keys_sqrd_lvl_* (:229-243) = this with the matching param_set. */
+int tae_generate_keys(int param_set, const uint8_t seed[32], int device, int threads,
+                      tae_client_key **client_key, tae_context **context);
+/* Client key only + standard-domain server keys exported to caller buffers (sizes from
+ * tae_server_key_sizes) -- used to broadcast keys across ranks before tae_context_create_raw. */
+int tae_server_key_sizes(int param_set, size_t *ksk_len, size_t *bsk_len, size_t *pfpksk_len);
+int tae_generate_keys_raw(int param_set, const uint8_t seed[32], int threads,
+                          tae_client_key **client_key, uint64_t *ksk, uint64_t *bsk,
+                          uint64_t *pfpksk);
+/* Server context from raw keys: mem = TAE_MEM_HOST (copied to the device) or TAE_MEM_DEVICE
+ * (device pointers on `device`, e.g. after an RCCL broadcast; they must outlive the context). */
+int tae_context_create_raw(int param_set, int device, const uint64_t *ksk, const uint64_t *bsk,
+                           const uint64_t *pfpksk, int mem, tae_context **context);
+void tae_context_free(tae_context *ctx);
+void tae_client_key_free(tae_client_key *ck);
+int tae_client_key_secrets(const tae_client_key *ck, uint64_t *lwe_sk /*[n]*/,
+                           uint64_t *glwe_sk /*[k*N]*/);
+int tae_context_params(const tae_context *ctx, tae_params *out);
+
+/* ---- ClientKeyT / ContextT (src/tfhe.rs:11-24) -------------------------------------------- */
+int tae_encrypt(const tae_client_key *ck, uint64_t bit, tae_bit **out);       /* ClientKey::encrypt */
+int tae_decrypt(const tae_client_key *ck, const tae_bit *bit, uint64_t *out); /* ClientKey::decrypt */
+int tae_trivial(const tae_context *ctx, uint64_t bit, tae_bit **out);         /* ContextT::trivial */
+/* raw: encrypt `count` bits with explicit encryption indices start..start+count ([count][K+1]) */
+int tae_encrypt_bits_raw(const tae_client_key *ck, const uint8_t *bits, size_t count,
+                         uint64_t start_index, uint64_t *out);
+int tae_decrypt_bits_raw(const tae_client_key *ck, const uint64_t *cts, size_t count, uint8_t *bits);
+
+/* ---- BitCt (shortint_woppbs_1bit.rs:26-151) ----------------------------------------------- */
+int tae_bit_clone(const tae_bit *bit, tae_bit **out);
+void tae_bit_free(tae_bit *bit);
+int tae_bit_xor_assign(tae_bit *lhs, const tae_bit *rhs); /* BitXorAssign (:134-142) */
+int tae_bit_noise_level(const tae_bit *bit, uint64_t *noise_level_squared);
+int tae_bit_data(const tae_bit *bit, uint64_t *out, size_t len); /* LWE coefficients [K+1] */
+int tae_bit_from_data(const tae_context *ctx, const uint64_t *data, size_t len,
+                      uint64_t noise_level_squared, tae_bit **out); /* BitCt::with_noise_level */
+
+/* ---- LUT + circuit bootstrap (shortint_woppbs_1bit.rs:274-336) ----------------------------- */
+/* generate_lookup_table: f_values[1 << input_bits] */
+int tae_generate_lookup_table(const tae_context *ctx, int input_bits, int output_bits,
+                              const uint64_t *f_values, tae_lut **out);
+void tae_lut_free(tae_lut *lut);
+int tae_lut_data(const tae_lut *lut, uint64_t *out, size_t len, size_t *needed);
+/* FheContext::circuit_bootstrap(&[&BitCt], &WopbsLUTBase) -> Vec<BitCt> */
+int tae_circuit_bootstrap(const tae_context *ctx, const tae_bit *const *bits, size_t n_bits,
+                          const tae_lut *lut, tae_bit **out /*[output_bits]*/);
+/* batched: groups x n_in bits [groups][n_in][K+1] -> [groups][n_out][K+1] */
+int tae_circuit_bootstrap_raw(const tae_context *ctx, const uint64_t *bits, size_t groups,
+                              int n_in, const tae_lut *lut, uint64_t *out, int mem);
+
+/* ---- Aes128Encrypt for ShortintWoppbs1BitSboxGalMulPbsAesEncrypt -------------------------
+ *      (src/aes_128/fhe.rs:16-38, fhe_impls/shortint_woppbs_1bit.rs:131-151,
+ *       fhe_sbox_gal_mul_pbs.rs:84-191) */
+/* encrypt_block_for_rounds: expanded_key[44*32] bits, block[128] bits, out[128] */
+int tae_aes_encrypt_block_for_rounds(const tae_context *ctx, const tae_bit *const *expanded_key,
+                                     const tae_bit *const *block, int rounds, tae_bit **out);
+/* batched extension of encrypt_block (main.rs:141-159 runs blocks in parallel) */
+int tae_aes_encrypt_blocks(const tae_context *ctx, const tae_bit *const *expanded_key,
+                           const tae_bit *const *blocks, size_t n_blocks, int rounds, tae_bit **out);
+/* key_schedule (fhe_sbox_gal_mul_pbs.rs:134-164): key[128] bits -> expanded[44*32] bits */
+int tae_aes_key_schedule(const tae_context *ctx, const tae_bit *const *key, tae_bit **expanded);
+/* raw arrays: rk [44*32][K+1], blocks [n][128][K+1], out [n][128][K+1]; inputs fresh
+ * (noise level 1) -- the noise schedule of the round function is validated statically. */
+int tae_aes_encrypt_blocks_raw(const tae_context *ctx, const uint64_t *rk, const uint64_t *blocks,
+                               size_t n_blocks, int rounds, uint64_t *out, int mem);
+
+/* ---- stage entry points (raw arrays; parity tests and profiling) ---------------------------- */
+int tae_stage_keyswitch(const tae_context *ctx, const uint64_t *in, size_t count, uint64_t *out, int mem);
+int tae_stage_pbs_shift_boolean(const tae_context *ctx, const uint64_t *small, size_t count, int level,
+                                uint64_t *big, int mem);
+int tae_stage_bootstrap(const tae_context *ctx, const uint64_t *small, size_t count,
+                        const uint64_t *lut_glwe, uint64_t *big, int mem);
+int tae_stage_pfks_ggsw(const tae_context *ctx, const uint64_t *big, size_t count, int level,
+                        uint64_t *ggsw, int mem);
+int tae_stage_ggsw_fourier(const tae_context *ctx, const uint64_t *ggsw, size_t count,
+                           double *ggsw_f /*complex interleaved*/, int mem);
+int tae_stage_vertical_packing(const tae_context *ctx, const double *ggsw_f, size_t groups, int n_in,
+                               const uint64_t *lut, int n_out, uint64_t *out, int mem);
+
+/* ---- device utilities -------------------------------------------------------------------- */
+int tae_synchronize(const tae_context *ctx);
+int tae_set_timing(const tae_context *ctx, int on);
+/* per-stage ms of the last batched call: [keyswitch, pbs, pfks, ggsw_fft, vp] */
+int tae_last_stage_times(const tae_context *ctx, float *ms5);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

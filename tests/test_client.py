@@ -1,0 +1,90 @@
+"""Host-side product logic on the CPU: keygen / encryption parity with the oracle (same keygen spec),
+LUT generation, BitCt noise bookkeeping (shortint_woppbs_1bit.rs:463-529), static AES noise schedule."""
+import numpy as np
+import pytest
+
+import tfhe_aes
+from tfhe_aes import Cleartext, aes_128
+
+
+def test_params_match_reference(oracle_mod):
+    # parameters.rs:29-205
+    for pid in range(4):
+        assert tfhe_aes.get_params(pid) == oracle_mod.params(pid)
+    p = tfhe_aes.get_params(tfhe_aes.PARAMS_SQRD_LVL_64)
+    assert (p["n"], p["k"], p["N"], p["pbs_l"], p["pbs_b"], p["ks_l"], p["ks_b"], p["cbs_l"], p["cbs_b"],
+            p["pfks_l"], p["pfks_b"], p["max_noise_sq"]) == (677, 4, 512, 3, 12, 4, 3, 1, 13, 2, 16, 64)
+
+
+def test_keygen_bit_identical_to_oracle(product_raw, oracle_keys):
+    ck, (ksk, bsk, pfpksk) = product_raw
+    lwe, glwe = ck.secrets()
+    assert np.array_equal(lwe, oracle_keys.lwe_sk())
+    assert np.array_equal(glwe, oracle_keys.glwe_sk())
+    oksk, obsk, opf = oracle_keys.raw_server()
+    assert np.array_equal(ksk, oksk)
+    assert np.array_equal(bsk, obsk)
+    assert np.array_equal(pfpksk, opf)
+
+
+def test_encrypt_matches_oracle_and_decrypts(product_raw, oracle_keys):
+    ck, _ = product_raw
+    bits = [0, 1, 1, 0, 1]
+    cts = ck.encrypt_bits_raw(bits, start_index=1000)
+    # the product encrypts with the key seed's ENCRYPT stream; the oracle restates it
+    from tests.conftest import SEED
+    ref = oracle_keys.encrypt_bits(bits, SEED, 1000)
+    assert np.array_equal(cts, ref)
+    assert list(ck.decrypt_bits_raw(cts)) == bits
+    assert list(oracle_keys.decrypt_bits(cts)) == bits
+
+
+def test_bit_encrypt_decrypt(product_raw):
+    ck, _ = product_raw
+    b1 = ck.encrypt(Cleartext(0))
+    b2 = ck.encrypt(Cleartext(1))
+    assert ck.decrypt(b1) == Cleartext(0)
+    assert ck.decrypt(b2) == Cleartext(1)
+
+
+def test_bit_xor(product_raw):
+    """test_bit_xor (:484-503) -- on lvl_64 keys (max noise^2 64)."""
+    ck, _ = product_raw
+    b1, b2, b3, b4 = (ck.encrypt(Cleartext(v)) for v in (0, 1, 0, 1))
+    assert ck.decrypt(b1 ^ b2) == Cleartext(1)
+    assert ck.decrypt(b1 ^ b3) == Cleartext(0)
+    assert ck.decrypt(b2 ^ b4) == Cleartext(0)
+    assert (b1 ^ b2).noise_level_squared == 2
+
+
+def test_bit_xor_above_max_noise():
+    """test_bit_xor_above_max_noise (:505-518): 5-way XOR at max noise^2 4 -> NoiseTooBig."""
+    ck, _ = tfhe_aes.generate_keys_raw(tfhe_aes.PARAMS_SQRD_LVL_4, bytes(32), threads=8)
+    b = [ck.encrypt(Cleartext(v)) for v in (0, 1, 0, 1, 0)]
+    acc = b[0] ^ b[1] ^ b[2] ^ b[3]
+    assert acc.noise_level_squared == 4
+    with pytest.raises(tfhe_aes.NoiseTooBig, match="NoiseTooBig"):
+        acc ^= b[4]
+
+
+def test_bit_xor_not_independent(product_raw):
+    """test_bit_xor_not_independent (:520-529)."""
+    ck, _ = product_raw
+    b1 = ck.encrypt(Cleartext(0))
+    with pytest.raises(tfhe_aes.NoiseNotIndependent, match="noise components not independent"):
+        _ = b1.clone() ^ b1.clone()
+
+
+def test_cleartext_out_of_bounds(product_raw):
+    ck, _ = product_raw
+    with pytest.raises(tfhe_aes.TaeError):
+        ck.encrypt(Cleartext(2))
+
+
+def test_no_gpu_means_no_context(product_raw):
+    """The product has no CPU fallback: without a GPU, building a server context fails loudly."""
+    if tfhe_aes.device_count() > 0:
+        pytest.skip("GPU present")
+    _, keys = product_raw
+    with pytest.raises(tfhe_aes.NoDevice):
+        tfhe_aes.context_from_raw(tfhe_aes.PARAMS_SQRD_LVL_64, keys)

@@ -1,0 +1,21 @@
+// AES-128 constants and byte-level helpers used by the FHE round driver.
+// Reference: src/aes_128.rs (SBOX :18-35, RC :37-39, ROUNDS :16, gf_256_mul :42-56),
+// src/aes_128/plain.rs:106-132 (key schedule, for host-side checks).
+#pragma once
+#include <cstdint>
+
+namespace tae {
+
+extern const uint8_t kSbox[256];
+extern const uint8_t kRcon[11];
+constexpr int kAesRounds = 10;
+
+// gf_256_mul exactly as the reference writes it, including its reduction quirk (it XORs 0x1b
+// when the high bit is CLEAR, aes_128.rs:50).  The x2/x3 LUT outputs inherit the quirk; the two
+// 0x1b terms cancel inside every MixColumns output, so full AES stays correct.
+uint8_t gf_256_mul(uint8_t a, uint8_t b);
+
+// plain key expansion into 176 bytes (word-major), plain.rs:106-132
+void plain_key_schedule(const uint8_t key[16], uint8_t rk[176]);
+
+}  // namespace tae

@@ -1,0 +1,499 @@
+// extern "C" boundary (include/tfhe_aes_gpu.h).  Each entry point maps a reference trait method
+// or tfhe-rs call to the host model (model.cpp) and the device Engine (kernels.hip); panics of the
+// reference become status codes, HIP failures TAE_E_HIP.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+
+#include "../../include/tfhe_aes_gpu.h"
+#include "client.hpp"
+#include "engine.hpp"
+#include "cplx.hpp"
+#include "model.hpp"
+
+struct tae_client_key {
+    tae::ClientKey ck;
+};
+struct tae_context {
+    std::unique_ptr<tae::Context> ctx;
+};
+struct tae_bit {
+    tae::BitCt b;
+};
+struct tae_lut {
+    tae::Lut l;
+};
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string &msg) {
+    g_last_error = msg;
+    return code;
+}
+
+template <class F>
+int guarded(F &&fn) {
+    try {
+        fn();
+        return TAE_OK;
+    } catch (const tae::ModelError &e) {
+        return fail(e.code, e.msg);
+    } catch (const tae::HipError &e) {
+        return fail(TAE_E_HIP, e.msg);
+    } catch (const std::bad_alloc &) {
+        return fail(TAE_E_ARG, "out of host memory");
+    } catch (const std::exception &e) {
+        return fail(TAE_E_PARAM, e.what());
+    }
+}
+
+void require(bool cond, const char *msg) {
+    if (!cond) throw tae::ModelError{TAE_E_ARG, msg};
+}
+
+tae::Params params_of(int param_set) {
+    tae::Params p;
+    if (!tae::get_params(param_set, p)) throw tae::ModelError{TAE_E_PARAM, "unknown parameter set"};
+    return p;
+}
+
+void fill(tae_params *o, const tae::Params &p) {
+    *o = {p.n, p.k, p.N, p.pbs_l, p.pbs_b, p.ks_l, p.ks_b, p.cbs_l, p.cbs_b, p.pfks_l, p.pfks_b,
+          p.lwe_std, p.glwe_std, p.pfks_std, p.max_noise_sq};
+}
+
+void require_device(int device) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
+        throw tae::ModelError{TAE_E_NODEV, "no GPU available: the HIP path has no CPU fallback"};
+    if (device < 0 || device >= count) throw tae::ModelError{TAE_E_NODEV, "device index out of range"};
+}
+
+std::vector<const tae::BitCt *> unwrap(const tae_bit *const *bits, size_t n) {
+    std::vector<const tae::BitCt *> v(n);
+    for (size_t i = 0; i < n; i++) {
+        require(bits[i] != nullptr, "null bit handle");
+        v[i] = &bits[i]->b;
+    }
+    return v;
+}
+
+// run `fn(d_in, d_out)` with host staging when mem == TAE_MEM_HOST
+template <class TI, class TO, class F>
+void staged(tae_context const *ctx, const TI *in, size_t in_bytes, TO *out, size_t out_bytes, int mem, F fn) {
+    tae::Context &c = *ctx->ctx;
+    std::lock_guard<std::mutex> g(c.mutex());
+    tae::Engine &e = c.engine();
+    tae::hip_check(hipSetDevice(e.device()), "hipSetDevice");
+    if (mem == TAE_MEM_DEVICE) {
+        fn(in, out);
+        e.synchronize();
+        return;
+    }
+    void *di = nullptr, *dout = nullptr;
+    tae::hip_check(hipMalloc(&di, std::max<size_t>(in_bytes, 16)), "hipMalloc");
+    if (hipMalloc(&dout, std::max<size_t>(out_bytes, 16)) != hipSuccess) {
+        hipFree(di);
+        throw tae::HipError{"hipMalloc"};
+    }
+    try {
+        tae::hip_check(hipMemcpy(di, in, in_bytes, hipMemcpyHostToDevice), "upload");
+        tae::hip_check(hipMemset(dout, 0, out_bytes), "memset");
+        fn(static_cast<const TI *>(di), static_cast<TO *>(dout));
+        e.synchronize();
+        tae::hip_check(hipMemcpy(out, dout, out_bytes, hipMemcpyDeviceToHost), "download");
+    } catch (...) {
+        hipFree(di);
+        hipFree(dout);
+        throw;
+    }
+    hipFree(di);
+    hipFree(dout);
+}
+
+void emit(const std::vector<tae::BitCt> &res, tae_bit **out) {
+    for (size_t i = 0; i < res.size(); i++) out[i] = new tae_bit{res[i]};
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *tae_last_error(void) { return g_last_error.c_str(); }
+const char *tae_version(void) { return "tfhe-aes-2_amd 0.1 (gfx950)"; }
+
+int tae_device_count(int *count) {
+    return guarded([&] {
+        require(count, "null");
+        *count = 0;
+        if (hipGetDeviceCount(count) != hipSuccess) *count = 0;
+    });
+}
+
+int tae_get_params(int param_set, tae_params *out) {
+    return guarded([&] {
+        require(out, "null");
+        fill(out, params_of(param_set));
+    });
+}
+
+int tae_server_key_sizes(int param_set, size_t *ksk_len, size_t *bsk_len, size_t *pfpksk_len) {
+    return guarded([&] {
+        const tae::Params p = params_of(param_set);
+        if (ksk_len) *ksk_len = p.ksk_len();
+        if (bsk_len) *bsk_len = p.bsk_len();
+        if (pfpksk_len) *pfpksk_len = p.pfpksk_len();
+    });
+}
+
+int tae_generate_keys_raw(int param_set, const uint8_t seed[32], int threads, tae_client_key **client_key,
+                          uint64_t *ksk, uint64_t *bsk, uint64_t *pfpksk) {
+    return guarded([&] {
+        require(seed && client_key, "null argument");
+        const tae::Params p = params_of(param_set);
+        auto ck = std::make_unique<tae_client_key>();
+        tae::ServerKeyRaw sk;
+        tae::generate_keys(p, seed, threads, ck->ck, sk);
+        if (ksk) std::memcpy(ksk, sk.ksk.data(), sk.ksk.size() * 8);
+        if (bsk) std::memcpy(bsk, sk.bsk.data(), sk.bsk.size() * 8);
+        if (pfpksk) std::memcpy(pfpksk, sk.pfpksk.data(), sk.pfpksk.size() * 8);
+        *client_key = ck.release();
+    });
+}
+
+int tae_generate_keys(int param_set, const uint8_t seed[32], int device, int threads, tae_client_key **client_key,
+                      tae_context **context) {
+    return guarded([&] {
+        require(seed && client_key && context, "null argument");
+        const tae::Params p = params_of(param_set);
+        require_device(device);
+        auto ck = std::make_unique<tae_client_key>();
+        tae::ServerKeyRaw sk;
+        tae::generate_keys(p, seed, threads, ck->ck, sk);
+        auto ctx = std::make_unique<tae_context>();
+        ctx->ctx = std::make_unique<tae::Context>(std::make_unique<tae::Engine>(sk, device));
+        *client_key = ck.release();
+        *context = ctx.release();
+    });
+}
+
+int tae_context_create_raw(int param_set, int device, const uint64_t *ksk, const uint64_t *bsk,
+                           const uint64_t *pfpksk, int mem, tae_context **context) {
+    return guarded([&] {
+        require(ksk && bsk && pfpksk && context, "null argument");
+        const tae::Params p = params_of(param_set);
+        require_device(device);
+        auto ctx = std::make_unique<tae_context>();
+        if (mem == TAE_MEM_DEVICE) {
+            ctx->ctx = std::make_unique<tae::Context>(std::make_unique<tae::Engine>(p, device, ksk, bsk, pfpksk));
+        } else {
+            tae::ServerKeyRaw sk;
+            sk.p = p;
+            sk.ksk.assign(ksk, ksk + p.ksk_len());
+            sk.bsk.assign(bsk, bsk + p.bsk_len());
+            sk.pfpksk.assign(pfpksk, pfpksk + p.pfpksk_len());
+            ctx->ctx = std::make_unique<tae::Context>(std::make_unique<tae::Engine>(sk, device));
+        }
+        *context = ctx.release();
+    });
+}
+
+void tae_context_free(tae_context *ctx) { delete ctx; }
+void tae_client_key_free(tae_client_key *ck) { delete ck; }
+
+int tae_client_key_secrets(const tae_client_key *ck, uint64_t *lwe_sk, uint64_t *glwe_sk) {
+    return guarded([&] {
+        require(ck, "null");
+        if (lwe_sk) std::memcpy(lwe_sk, ck->ck.lwe_sk.data(), ck->ck.lwe_sk.size() * 8);
+        if (glwe_sk) std::memcpy(glwe_sk, ck->ck.glwe_sk.data(), ck->ck.glwe_sk.size() * 8);
+    });
+}
+
+int tae_context_params(const tae_context *ctx, tae_params *out) {
+    return guarded([&] {
+        require(ctx && out, "null");
+        fill(out, ctx->ctx->params());
+    });
+}
+
+int tae_encrypt(const tae_client_key *ck, uint64_t bit, tae_bit **out) {
+    return guarded([&] {
+        require(ck && out, "null");
+        if (bit > 1) throw tae::ModelError{TAE_E_ARG, "cleartext out of bounds: " + std::to_string(bit)};
+        auto &c = const_cast<tae_client_key *>(ck)->ck;
+        auto b = std::make_unique<tae_bit>();
+        b->b.ct.assign(c.p.big_len(), 0);
+        c.encrypt_bit_at(bit, c.next_index.fetch_add(1), b->b.ct.data());
+        b->b.noise = tae::NoiseLevel::with_noise_level(1, tae::next_ct_id());  // BitCt::fresh
+        b->b.max_noise_sq = c.p.max_noise_sq;
+        *out = b.release();
+    });
+}
+
+int tae_decrypt(const tae_client_key *ck, const tae_bit *bit, uint64_t *out) {
+    return guarded([&] {
+        require(ck && bit && out, "null");
+        require(bit->b.ct.size() == ck->ck.p.big_len(), "ciphertext size mismatch");
+        *out = ck->ck.decrypt_bit(bit->b.ct.data());
+    });
+}
+
+int tae_trivial(const tae_context *ctx, uint64_t bit, tae_bit **out) {
+    return guarded([&] {
+        require(ctx && out, "null");
+        *out = new tae_bit{ctx->ctx->trivial(bit)};
+    });
+}
+
+int tae_encrypt_bits_raw(const tae_client_key *ck, const uint8_t *bits, size_t count, uint64_t start_index,
+                         uint64_t *out) {
+    return guarded([&] {
+        require(ck && (bits || !count) && (out || !count), "null");
+        const size_t L = ck->ck.p.big_len();
+        for (size_t i = 0; i < count; i++) {
+            require(bits[i] < 2, "cleartext out of bounds");
+            ck->ck.encrypt_bit_at(bits[i], start_index + i, out + i * L);
+        }
+    });
+}
+
+int tae_decrypt_bits_raw(const tae_client_key *ck, const uint64_t *cts, size_t count, uint8_t *bits) {
+    return guarded([&] {
+        require(ck && (cts || !count) && (bits || !count), "null");
+        const size_t L = ck->ck.p.big_len();
+        for (size_t i = 0; i < count; i++) bits[i] = (uint8_t)ck->ck.decrypt_bit(cts + i * L);
+    });
+}
+
+int tae_bit_clone(const tae_bit *bit, tae_bit **out) {
+    return guarded([&] {
+        require(bit && out, "null");
+        *out = new tae_bit{bit->b};
+    });
+}
+
+void tae_bit_free(tae_bit *bit) { delete bit; }
+
+int tae_bit_xor_assign(tae_bit *lhs, const tae_bit *rhs) {
+    return guarded([&] {
+        require(lhs && rhs, "null");
+        lhs->b.xor_assign(rhs->b);
+    });
+}
+
+int tae_bit_noise_level(const tae_bit *bit, uint64_t *nl) {
+    return guarded([&] {
+        require(bit && nl, "null");
+        *nl = bit->b.noise.noise_level_squared;
+    });
+}
+
+int tae_bit_data(const tae_bit *bit, uint64_t *out, size_t len) {
+    return guarded([&] {
+        require(bit && out, "null");
+        require(len == bit->b.ct.size(), "length mismatch");
+        std::memcpy(out, bit->b.ct.data(), len * 8);
+    });
+}
+
+int tae_bit_from_data(const tae_context *ctx, const uint64_t *data, size_t len, uint64_t nl, tae_bit **out) {
+    return guarded([&] {
+        require(ctx && data && out, "null");
+        require(len == ctx->ctx->params().big_len(), "length mismatch");
+        *out = new tae_bit{ctx->ctx->wrap(std::vector<uint64_t>(data, data + len), nl)};
+    });
+}
+
+int tae_generate_lookup_table(const tae_context *ctx, int input_bits, int output_bits, const uint64_t *f_values,
+                              tae_lut **out) {
+    return guarded([&] {
+        require(ctx && f_values && out, "null");
+        *out = new tae_lut{ctx->ctx->generate_lookup_table(input_bits, output_bits, f_values)};
+    });
+}
+
+void tae_lut_free(tae_lut *lut) { delete lut; }
+
+int tae_lut_data(const tae_lut *lut, uint64_t *out, size_t len, size_t *needed) {
+    return guarded([&] {
+        require(lut, "null");
+        if (needed) *needed = lut->l.data.size();
+        if (out) {
+            require(len == lut->l.data.size(), "length mismatch");
+            std::memcpy(out, lut->l.data.data(), len * 8);
+        }
+    });
+}
+
+int tae_circuit_bootstrap(const tae_context *ctx, const tae_bit *const *bits, size_t n_bits, const tae_lut *lut,
+                          tae_bit **out) {
+    return guarded([&] {
+        require(ctx && bits && lut && out, "null");
+        emit(ctx->ctx->circuit_bootstrap(unwrap(bits, n_bits), lut->l), out);
+    });
+}
+
+int tae_circuit_bootstrap_raw(const tae_context *ctx, const uint64_t *bits, size_t groups, int n_in,
+                              const tae_lut *lut, uint64_t *out, int mem) {
+    return guarded([&] {
+        require(ctx && bits && lut && out, "null");
+        ctx->ctx->circuit_bootstrap_raw(bits, groups, n_in, lut->l, out, mem == TAE_MEM_DEVICE);
+    });
+}
+
+int tae_aes_encrypt_block_for_rounds(const tae_context *ctx, const tae_bit *const *expanded_key,
+                                     const tae_bit *const *block, int rounds, tae_bit **out) {
+    return guarded([&] {
+        require(ctx && expanded_key && block && out, "null");
+        emit(ctx->ctx->aes_encrypt_blocks(unwrap(expanded_key, 44 * 32), unwrap(block, 128), 1, rounds), out);
+    });
+}
+
+int tae_aes_encrypt_blocks(const tae_context *ctx, const tae_bit *const *expanded_key, const tae_bit *const *blocks,
+                           size_t n_blocks, int rounds, tae_bit **out) {
+    return guarded([&] {
+        require(ctx && expanded_key && blocks && out, "null");
+        emit(ctx->ctx->aes_encrypt_blocks(unwrap(expanded_key, 44 * 32), unwrap(blocks, 128 * n_blocks), n_blocks,
+                                          rounds),
+             out);
+    });
+}
+
+int tae_aes_key_schedule(const tae_context *ctx, const tae_bit *const *key, tae_bit **expanded) {
+    return guarded([&] {
+        require(ctx && key && expanded, "null");
+        emit(ctx->ctx->aes_key_schedule(unwrap(key, 128)), expanded);
+    });
+}
+
+int tae_aes_encrypt_blocks_raw(const tae_context *ctx, const uint64_t *rk, const uint64_t *blocks, size_t n_blocks,
+                               int rounds, uint64_t *out, int mem) {
+    return guarded([&] {
+        require(ctx && rk && blocks && out, "null");
+        ctx->ctx->aes_encrypt_blocks_raw(rk, blocks, n_blocks, rounds, out, mem == TAE_MEM_DEVICE);
+    });
+}
+
+
+int tae_stage_keyswitch(const tae_context *ctx, const uint64_t *in, size_t count, uint64_t *out, int mem) {
+    return guarded([&] {
+        require(ctx && in && out, "null");
+        const auto &p = ctx->ctx->params();
+        staged(ctx, in, count * p.big_len() * 8, out, count * p.small_len() * 8, mem,
+               [&](const uint64_t *a, uint64_t *b) { ctx->ctx->engine().keyswitch(a, b, count); });
+    });
+}
+
+int tae_stage_pbs_shift_boolean(const tae_context *ctx, const uint64_t *small, size_t count, int level, uint64_t *big,
+                                int mem) {
+    return guarded([&] {
+        require(ctx && small && big, "null");
+        const auto &p = ctx->ctx->params();
+        require(level >= 1 && level <= p.cbs_l, "level out of range");
+        staged(ctx, small, count * p.small_len() * 8, big, count * p.big_len() * 8, mem,
+               [&](const uint64_t *a, uint64_t *b) { ctx->ctx->engine().pbs_shift_boolean(a, b, count, level); });
+    });
+}
+
+int tae_stage_bootstrap(const tae_context *ctx, const uint64_t *small, size_t count, const uint64_t *lut_glwe,
+                        uint64_t *big, int mem) {
+    return guarded([&] {
+        require(ctx && small && lut_glwe && big, "null");
+        const auto &p = ctx->ctx->params();
+        void *d_lut = nullptr;
+        const uint64_t *lut = lut_glwe;
+        if (mem != TAE_MEM_DEVICE) {
+            tae::hip_check(hipMalloc(&d_lut, p.glwe_len() * 8), "hipMalloc");
+            tae::hip_check(hipMemcpy(d_lut, lut_glwe, p.glwe_len() * 8, hipMemcpyHostToDevice), "upload");
+            lut = static_cast<const uint64_t *>(d_lut);
+        }
+        try {
+            staged(ctx, small, count * p.small_len() * 8, big, count * p.big_len() * 8, mem,
+                   [&](const uint64_t *a, uint64_t *b) { ctx->ctx->engine().bootstrap(a, lut, b, count, 0, 0); });
+        } catch (...) {
+            if (d_lut) hipFree(d_lut);
+            throw;
+        }
+        if (d_lut) hipFree(d_lut);
+    });
+}
+
+int tae_stage_pfks_ggsw(const tae_context *ctx, const uint64_t *big, size_t count, int level, uint64_t *ggsw, int mem) {
+    return guarded([&] {
+        require(ctx && big && ggsw, "null");
+        const auto &p = ctx->ctx->params();
+        require(level >= 1 && level <= p.cbs_l, "level out of range");
+        staged(ctx, big, count * p.big_len() * 8, ggsw, count * p.cbs_ggsw_len() * 8, mem,
+               [&](const uint64_t *a, uint64_t *b) { ctx->ctx->engine().pfks_into_ggsw(a, b, count, level); });
+    });
+}
+
+int tae_stage_ggsw_fourier(const tae_context *ctx, const uint64_t *ggsw, size_t count, double *ggsw_f, int mem) {
+    return guarded([&] {
+        require(ctx && ggsw && ggsw_f, "null");
+        const auto &p = ctx->ctx->params();
+        staged(ctx, ggsw, count * p.cbs_ggsw_len() * 8, ggsw_f, count * p.cbs_ggsw_fourier_len() * 16, mem,
+               [&](const uint64_t *a, double *b) {
+                   ctx->ctx->engine().ggsw_to_fourier(a, reinterpret_cast<tae::cplx *>(b), count);
+               });
+    });
+}
+
+int tae_stage_vertical_packing(const tae_context *ctx, const double *ggsw_f, size_t groups, int n_in,
+                               const uint64_t *lut, int n_out, uint64_t *out, int mem) {
+    return guarded([&] {
+        require(ctx && ggsw_f && lut && out, "null");
+        const auto &p = ctx->ctx->params();
+        void *d_lut = nullptr;
+        const uint64_t *l = lut;
+        if (mem != TAE_MEM_DEVICE) {
+            tae::hip_check(hipMalloc(&d_lut, (size_t)n_out * p.N * 8), "hipMalloc");
+            tae::hip_check(hipMemcpy(d_lut, lut, (size_t)n_out * p.N * 8, hipMemcpyHostToDevice), "upload");
+            l = static_cast<const uint64_t *>(d_lut);
+        }
+        try {
+            staged(ctx, ggsw_f, groups * n_in * p.cbs_ggsw_fourier_len() * 16, out, groups * n_out * p.big_len() * 8,
+                   mem, [&](const double *a, uint64_t *b) {
+                       ctx->ctx->engine().vertical_packing(reinterpret_cast<const tae::cplx *>(a), groups, n_in, l,
+                                                           n_out, b);
+                   });
+        } catch (...) {
+            if (d_lut) hipFree(d_lut);
+            throw;
+        }
+        if (d_lut) hipFree(d_lut);
+    });
+}
+
+int tae_synchronize(const tae_context *ctx) {
+    return guarded([&] {
+        require(ctx, "null");
+        ctx->ctx->engine().synchronize();
+    });
+}
+
+int tae_set_timing(const tae_context *ctx, int on) {
+    return guarded([&] {
+        require(ctx, "null");
+        ctx->ctx->engine().set_timing(on != 0);
+    });
+}
+
+int tae_last_stage_times(const tae_context *ctx, float *ms5) {
+    return guarded([&] {
+        require(ctx && ms5, "null");
+        const auto &t = ctx->ctx->engine().last_times();
+        ms5[0] = t.keyswitch;
+        ms5[1] = t.pbs;
+        ms5[2] = t.pfks;
+        ms5[3] = t.ggsw_fft;
+        ms5[4] = t.vertical_packing;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,80 @@
+// Client side of the 1-bit WoP-PBS model: key generation, bit encryption/decryption, LUTs.
+//
+// Reference: src/tfhe/shortint_woppbs_1bit.rs
+//   ClientKey::{encrypt, decrypt}            :197-226
+//   FheContext::generate_keys_with_params    :245-268 (tfhe::shortint::gen_keys +
+//                                             WopbsKey::new_wopbs_key_only_for_wopbs)
+//   encode_bit / decode_bit                  :125-132
+//   generate_multivariate_luts               :366-403
+// The reference seeds its CSPRNG from the OS (src/tfhe/engine.rs:164-168); this build draws all
+// randomness from ChaCha20(seed) streams laid out as in DESIGN.md ("keygen spec") so that a run is
+// reproducible and the CPU oracle can regenerate identical keys.
+#pragma once
+#include <array>
+#include <atomic>
+#include <cstdint>
+#include <vector>
+
+#include "params.hpp"
+
+namespace tae {
+
+// ---- ChaCha20 (DJB: 64-bit block counter, 64-bit nonce) ----
+void chacha20_block(const uint8_t key[32], uint64_t nonce, uint64_t counter, uint8_t out[64]);
+
+class ChaChaStream {
+  public:
+    ChaChaStream(const uint8_t key[32], uint64_t nonce, uint64_t counter);
+    uint64_t next_u64();
+    uint64_t next_gaussian_torus(double sigma);  // Box-Muller, rint(z * sigma * 2^64)
+  private:
+    uint8_t key_[32];
+    uint64_t nonce_, ctr_;
+    uint8_t buf_[64];
+    int pos_;
+};
+
+// Keygen stream purposes (DESIGN.md keygen spec).
+enum Purpose : uint64_t { LWE_SK = 1, GLWE_SK = 2, KSK = 3, BSK = 4, PFPKSK = 5, ENCRYPT = 6 };
+constexpr uint64_t kCtStride = 1ull << 24;
+
+inline uint64_t encode_bit(uint64_t bit) { return bit << 63; }
+inline uint64_t decode_bit(uint64_t x) { return ((x + (1ull << 62)) & (1ull << 63)) >> 63; }
+
+// Standard-domain server keys (what tfhe's WopbsKey holds before the Fourier conversion).
+struct ServerKeyRaw {
+    Params p;
+    std::vector<uint64_t> ksk;     // [K][ks_l][n+1]
+    std::vector<uint64_t> bsk;     // [n][pbs_l][k+1][(k+1)N]
+    std::vector<uint64_t> pfpksk;  // [k+1][K+1][pfks_l][(k+1)N]
+};
+
+struct ClientKey {
+    Params p;
+    std::array<uint8_t, 32> seed;
+    std::vector<uint64_t> lwe_sk;   // [n]
+    std::vector<uint64_t> glwe_sk;  // [K] (GLWE key as LWE key of dimension K)
+    std::atomic<uint64_t> next_index{0};
+
+    // ClientKey::encrypt: LWE under the big key, lwe noise, encode_bit (encryption index explicit)
+    void encrypt_bit_at(uint64_t bit, uint64_t index, uint64_t *out) const;
+    uint64_t phase(const uint64_t *ct) const;
+    uint64_t decrypt_bit(const uint64_t *ct) const { return decode_bit(phase(ct)); }
+};
+
+// generate_keys_with_params; threads = worker threads for the key material.
+void generate_keys(const Params &p, const uint8_t seed[32], int threads, ClientKey &ck,
+                   ServerKeyRaw &sk);
+
+// generate_multivariate_luts: out [output_bits][N << tree_bits]
+size_t lut_small_len(int N, int input_bits);
+void generate_lut(int N, int input_bits, int output_bits, const uint64_t *f_table, uint64_t *out);
+
+// Negacyclic FFT tables (twist, untwist, W_M) -- the spec shared with the kernels.
+struct FftTables {
+    int N, M;
+    std::vector<double> twist, untwist, w;  // interleaved (re, im), M entries each
+};
+FftTables make_fft_tables(int N);
+
+}  // namespace tae

@@ -1,0 +1,115 @@
+// Device engine: server keys resident in HBM and the batched hot-path stages as HIP kernels.
+//
+// Reference hot path: FheContext::circuit_bootstrap
+// (src/tfhe/shortint_woppbs_1bit.rs:292-336) = per input bit extract_dual_bit_from_bit
+// (:339-363 -> tfhe extract_bits = one LWE keyswitch), then tfhe
+// circuit_bootstrap_boolean_vertical_packing (homomorphic_shift_boolean PBS, k+1 private
+// functional keyswitches into a GGSW, forward FFT of the GGSW, vertical-packing blind rotation,
+// sample extraction).  Every stage here is batched over all bits of all SBOXes of a round.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "client.hpp"
+#include "cplx.hpp"
+#include "params.hpp"
+
+namespace tae {
+
+struct HipError {
+    std::string msg;
+};
+
+void hip_check(hipError_t e, const char *what);
+
+// Timing of the most recent batched call, per stage (ms, HIP events on the engine stream).
+struct StageTimes {
+    float keyswitch = 0, pbs = 0, pfks = 0, ggsw_fft = 0, vertical_packing = 0, linear = 0;
+    int pbs_launches = 0;
+};
+
+class Engine {
+  public:
+    // Uploads the standard-domain keys and converts the BSK to the Fourier domain on device.
+    Engine(const ServerKeyRaw &keys, int device);
+    // Attach to keys already resident on this device (e.g. broadcast over RCCL); the standard
+    // BSK is converted in place into an engine-owned Fourier buffer.  Pointers must stay valid.
+    Engine(const Params &p, int device, const uint64_t *d_ksk, const uint64_t *d_bsk,
+           const uint64_t *d_pfpksk);
+    ~Engine();
+    Engine(const Engine &) = delete;
+    Engine &operator=(const Engine &) = delete;
+
+    const Params &params() const { return p_; }
+    int device() const { return device_; }
+    hipStream_t stream() const { return stream_; }
+
+    // ---- batched stages, all pointers device-resident ----
+    // keyswitch_lwe_ciphertext: [B][K+1] -> [B][n+1]
+    void keyswitch(const uint64_t *d_in, uint64_t *d_out, size_t B);
+    // homomorphic_shift_boolean at cbs level `level`: [B][n+1] -> [B][K+1]
+    void pbs_shift_boolean(const uint64_t *d_small, uint64_t *d_big, size_t B, int level);
+    // generic FourierLweBootstrapKey::bootstrap with a per-batch LUT GLWE [(k+1)N]
+    void bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint64_t *d_big, size_t B,
+                   uint64_t body_add, uint64_t out_add);
+    // private functional keyswitches of level `level`: [B][K+1] -> GGSW rows of that level in
+    // d_ggsw [B][cbs_l][k+1][(k+1)N]
+    void pfks_into_ggsw(const uint64_t *d_big, uint64_t *d_ggsw, size_t B, int level);
+    // fill_with_forward_fourier: [B][cbs_l][k+1][(k+1)N] -> [B][cbs_l][k+1][k+1][M]
+    void ggsw_to_fourier(const uint64_t *d_ggsw, cplx *d_ggsw_f, size_t B);
+    // vertical_packing for each group of n_in GGSWs: d_ggsw_f [G][n_in][...], d_lut
+    // [n_out][N], out [G][n_out][K+1]
+    void vertical_packing(const cplx *d_ggsw_f, size_t G, int n_in, const uint64_t *d_lut, int n_out,
+                          uint64_t *d_out);
+    // FheContext::circuit_bootstrap over G groups: bits [G][n_in][K+1] -> [G][n_out][K+1]
+    void circuit_bootstrap(const uint64_t *d_bits, size_t G, int n_in, const uint64_t *d_lut,
+                           int n_out, uint64_t *d_out);
+
+    // ---- AES driver (fhe_sbox_gal_mul_pbs::encrypt_block_for_rounds over many blocks) ----
+    // rk [44*32][K+1] (expanded key words, word-major, MSB-first bits), blocks [nb][128][K+1]
+    void aes_encrypt_blocks(const uint64_t *d_rk, const uint64_t *d_blocks, size_t nb, int rounds,
+                            uint64_t *d_out);
+
+    // ---- element-wise helpers ----
+    void lwe_add(uint64_t *d_a, const uint64_t *d_b, size_t count);  // a += b (count u64)
+
+    void synchronize();
+    const StageTimes &last_times() const { return times_; }
+    void set_timing(bool on) { timing_ = on; }
+
+    // scratch sizing: reserve buffers for a circuit_bootstrap of `bits` input bits
+    void reserve(size_t bits, size_t outputs);
+
+    const uint64_t *lut_galmul() const { return d_lut24_; }  // 8 -> 24 (S, 2S', 3S')
+    const uint64_t *lut_sbox() const { return d_lut8_; }     // 8 -> 8 SBOX
+
+  private:
+    void init_common();
+    void bsk_to_fourier(const uint64_t *d_bsk_std);
+    void *alloc(size_t bytes);
+    template <class T>
+    T *grow(T *&ptr, size_t &cap, size_t count);
+
+    Params p_;
+    int device_;
+    hipStream_t stream_ = nullptr;
+    bool owns_keys_ = false;
+    uint64_t *d_ksk_ = nullptr, *d_pfpksk_ = nullptr;
+    cplx *d_bsk_f_ = nullptr;
+    cplx *d_twist_ = nullptr, *d_untwist_ = nullptr, *d_w_ = nullptr;
+    uint64_t *d_lut_shift_ = nullptr;  // per cbs level: trivial GLWE with body = -alpha
+    uint64_t *d_lut24_ = nullptr, *d_lut8_ = nullptr;
+    // scratch
+    uint64_t *d_small_ = nullptr, *d_big_ = nullptr, *d_ggsw_ = nullptr, *d_state_ = nullptr,
+             *d_muls_ = nullptr;
+    cplx *d_ggsw_f_ = nullptr;
+    size_t cap_small_ = 0, cap_big_ = 0, cap_ggsw_ = 0, cap_ggsw_f_ = 0, cap_state_ = 0, cap_muls_ = 0;
+    hipEvent_t ev_[8];
+    bool timing_ = false;
+    StageTimes times_;
+};
+
+}  // namespace tae

@@ -1,0 +1,160 @@
+// Negacyclic f64 FFT building blocks for CDNA4 (gfx950).
+//
+// Math (tfhe-fft 0.7 as used by tfhe-rs fft64, Cargo.lock:773): a real polynomial p of size N is
+// folded to z_j = (p_j + i p_{j+M}) * e^{i pi j / N}, M = N/2, and transformed with an M-point
+// DFT; the backward path runs the inverse DFT, multiplies by conj(twist)/M and takes the
+// fractional part of the torus value (UnsignedTorus::from_torus).
+//
+// Schedule: decimation-in-frequency, radix R (R=16 for M=256, R=8 for M=512), P passes, so the
+// spectrum lives in digit-reversed order; the inverse is the mirrored decimation-in-time.  Every
+// f64 operation is fixed (explicit fma, -ffp-contract=off), so the CPU oracle can restate the
+// schedule and compare ciphertexts bit-exactly.  A pass is done by M/R threads ("TPJ" threads per
+// polynomial), each holding R complex values in registers; passes exchange through LDS.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "cplx.hpp"
+
+namespace tae {
+
+__device__ __forceinline__ cplx cmul(cplx a, cplx b) {
+    return {fma(a.re, b.re, -(a.im * b.im)), fma(a.re, b.im, a.im * b.re)};
+}
+__device__ __forceinline__ cplx cconj(cplx a) { return {a.re, -a.im}; }
+__device__ __forceinline__ cplx cadd(cplx a, cplx b) { return {a.re + b.re, a.im + b.im}; }
+__device__ __forceinline__ cplx csub(cplx a, cplx b) { return {a.re - b.re, a.im - b.im}; }
+
+template <int M>
+struct FftPlan;
+template <>
+struct FftPlan<256> {
+    static constexpr int R = 16, P = 2;
+};
+template <>
+struct FftPlan<512> {
+    static constexpr int R = 8, P = 3;
+};
+
+template <bool INV>
+__device__ __forceinline__ void dft4(cplx &a, cplx &b, cplx &c, cplx &d) {
+    const cplx t0 = cadd(a, c), t1 = csub(a, c), t2 = cadd(b, d), t3 = csub(b, d);
+    a = cadd(t0, t2);
+    c = csub(t0, t2);
+    if (!INV) {
+        b = {t1.re + t3.im, t1.im - t3.re};
+        d = {t1.re - t3.im, t1.im + t3.re};
+    } else {
+        b = {t1.re - t3.im, t1.im + t3.re};
+        d = {t1.re + t3.im, t1.im - t3.re};
+    }
+}
+
+// x * W_R^e (W_R = e^{-2 pi i / R}, conjugated for the inverse); e == R/4 is the exact -i / +i
+template <int R, int M, bool INV>
+__device__ __forceinline__ cplx tw_small(cplx x, int e, const cplx *__restrict__ w) {
+    if (e == 0) return x;
+    if (4 * e == R) return INV ? cplx{-x.im, x.re} : cplx{x.im, -x.re};
+    const cplx t = w[e * (M / R)];
+    return cmul(x, INV ? cconj(t) : t);
+}
+
+// In-register R-point DFT in natural order.  DFT16 = 4x4 (x[n1 + 4 n2] -> X[k1 + 4 k2]),
+// DFT8 = 2x4 (x[n1 + 2 n2] -> X[k1 + 4 k2]).
+template <int R, int M, bool INV>
+__device__ __forceinline__ void dft(cplx *v, const cplx *__restrict__ w) {
+    if constexpr (R == 16) {
+        cplx y[16];
+#pragma unroll
+        for (int n1 = 0; n1 < 4; n1++) dft4<INV>(v[n1], v[n1 + 4], v[n1 + 8], v[n1 + 12]);
+#pragma unroll
+        for (int n1 = 0; n1 < 4; n1++)
+#pragma unroll
+            for (int k1 = 0; k1 < 4; k1++) y[4 * k1 + n1] = tw_small<16, M, INV>(v[n1 + 4 * k1], n1 * k1, w);
+#pragma unroll
+        for (int k1 = 0; k1 < 4; k1++) dft4<INV>(y[4 * k1], y[4 * k1 + 1], y[4 * k1 + 2], y[4 * k1 + 3]);
+#pragma unroll
+        for (int k1 = 0; k1 < 4; k1++)
+#pragma unroll
+            for (int k2 = 0; k2 < 4; k2++) v[k1 + 4 * k2] = y[4 * k1 + k2];
+    } else {
+        static_assert(R == 8, "radix");
+        cplx y[8];
+#pragma unroll
+        for (int n1 = 0; n1 < 2; n1++) dft4<INV>(v[n1], v[n1 + 2], v[n1 + 4], v[n1 + 6]);
+#pragma unroll
+        for (int n1 = 0; n1 < 2; n1++)
+#pragma unroll
+            for (int k1 = 0; k1 < 4; k1++) y[2 * k1 + n1] = tw_small<8, M, INV>(v[n1 + 2 * k1], n1 * k1, w);
+#pragma unroll
+        for (int k1 = 0; k1 < 4; k1++) {
+            const cplx a = y[2 * k1], b = y[2 * k1 + 1];
+            v[k1] = cadd(a, b);
+            v[k1 + 4] = csub(a, b);
+        }
+    }
+}
+
+// ---- torus helpers (tfhe-rs SignedDecomposer, UnsignedTorus::from_torus) ----
+
+// digit of level `lev` (1 = most significant) of the balanced base-2^B decomposition
+__device__ __forceinline__ int64_t decomp_digit(uint64_t x, int base_log, int levels, int lev) {
+    const int nrb = 64 - base_log * levels;
+    uint64_t r = x >> (nrb - 1);
+    r += r & 1;
+    r >>= 1;  // = closest_representable(x) >> nrb
+    uint64_t state = r;
+    const uint64_t mask = (1ull << base_log) - 1;
+    int64_t digit = 0;
+    for (int l = levels; l >= lev; l--) {
+        const uint64_t res = state & mask;
+        state >>= base_log;
+        uint64_t carry = ((res - 1) | state) & res;
+        carry >>= (base_log - 1);
+        state += carry;
+        digit = (int64_t)(res - (carry << base_log));
+    }
+    return digit;
+}
+
+__device__ __forceinline__ uint64_t from_torus(double x) {
+    const double f = x - round(x);
+    const double v = round(f * 0x1p64);
+    const int64_t iv = v >= 0x1p63 ? INT64_MAX : (int64_t)v;
+    return (uint64_t)iv;
+}
+
+// pbs_modulus_switch: round(x * 2N / 2^64) in [0, 2N]
+__device__ __forceinline__ int mod_switch(uint64_t x, int logN) {
+    uint64_t o = x >> (64 - logN - 2);
+    o += o & 1;
+    return (int)(o >> 1);
+}
+
+// coefficient j of poly * X^e (e in [0, 2N)): poly[src] with sign
+__device__ __forceinline__ uint64_t rotated_coeff(const uint64_t *poly, int j, int e, int N) {
+    int src = j - e;
+    bool neg = false;
+    if (src < 0) {
+        src += N;
+        neg = !neg;
+    }
+    if (src < 0) {
+        src += N;
+        neg = !neg;
+    }
+    const uint64_t v = poly[src];
+    return neg ? (0 - v) : v;
+}
+
+// (uint64)(int64)d * key mod 2^64 with 32-bit multiplies
+__device__ __forceinline__ uint64_t mul_i32_u64(int32_t d, uint64_t key) {
+    const uint32_t lo = (uint32_t)key, hi = (uint32_t)(key >> 32);
+    const uint32_t du = (uint32_t)d;
+    const uint64_t p = (uint64_t)lo * du;
+    const uint32_t h = hi * du - (d < 0 ? lo : 0u);
+    return p + ((uint64_t)h << 32);
+}
+
+}  // namespace tae

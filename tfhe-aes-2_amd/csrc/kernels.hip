@@ -1,0 +1,680 @@
+// HIP kernels for gfx950 (CDNA4) and the Engine that drives them.
+//
+// Hot path, batched over every input bit of every SBOX of a round:
+//   keyswitch_kernel      tfhe keyswitch_lwe_ciphertext            (extract_dual_bit_from_bit,
+//                                                                   shortint_woppbs_1bit.rs:339-363)
+//   blind_rotate_kernel   tfhe FourierLweBootstrapKey::bootstrap   (homomorphic_shift_boolean)
+//                         tfhe wop_pbs::vertical_packing           (blind_rotate_assign, VP flavour)
+//   pfks_kernel           tfhe private_functional_keyswitch_lwe_ciphertext_into_glwe_ciphertext
+//   fft_torus_kernel      tfhe FourierGgswCiphertext::fill_with_forward_fourier (and the BSK)
+//   aes_*_kernel          ShiftRows / MixColumns / AddRoundKey as LWE additions
+//                         (fhe_sbox_gal_mul_pbs.rs:61-132, data_model.rs:270-281)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+
+#include "aes.hpp"
+#include "engine.hpp"
+#include "fft_device.hpp"
+
+namespace tae {
+
+void hip_check(hipError_t e, const char *what) {
+    if (e != hipSuccess) throw HipError{std::string(what) + ": " + hipGetErrorString(e)};
+}
+#define HIPC(x) hip_check((x), #x)
+
+namespace {
+
+constexpr int kThreads = 256;
+
+// ---------------------------------------------------------------------------------------------
+// External product on an LDS-resident GLWE accumulator:
+//   acc += GGSW [x] (acc * X^e - acc)          (cmux(ct0 = acc, ct1 = acc * X^e, ggsw))
+// GGSW Fourier layout [lev-1][row p][col c][M]; rows consumed finest level first, p ascending
+// (fft64 add_external_product_assign: ggsw.into_levels().rev() zipped with the decomposition).
+// ---------------------------------------------------------------------------------------------
+template <int N>
+__device__ void ext_product_step(uint64_t *__restrict__ acc, cplx *__restrict__ X, cplx *__restrict__ Y,
+                                 int e, const cplx *__restrict__ ggsw, int k, int levels, int base_log,
+                                 const cplx *__restrict__ twist, const cplx *__restrict__ untwist,
+                                 const cplx *__restrict__ w) {
+    constexpr int M = N / 2;
+    constexpr int R = FftPlan<M>::R, P = FftPlan<M>::P, TPJ = M / R;
+    const int tid = threadIdx.x;
+    const int rows = (k + 1) * levels;
+
+    // ---- forward pass 0: rotated difference, decomposition, twist, DFT_R, twiddles ----
+    for (int jt = tid; jt < rows * TPJ; jt += blockDim.x) {
+        const int r = jt / TPJ, u = jt - r * TPJ;
+        const int p = r % (k + 1), lev = r / (k + 1) + 1;
+        const uint64_t *poly = acc + p * N;
+        cplx v[R];
+#pragma unroll
+        for (int m = 0; m < R; m++) {
+            const int j = u + m * TPJ;
+            const uint64_t d0 = rotated_coeff(poly, j, e, N) - poly[j];
+            const uint64_t d1 = rotated_coeff(poly, j + M, e, N) - poly[j + M];
+            const double x0 = (double)decomp_digit(d0, base_log, levels, lev);
+            const double x1 = (double)decomp_digit(d1, base_log, levels, lev);
+            const cplx t = twist[j];
+            v[m] = {fma(x0, t.re, -(x1 * t.im)), fma(x0, t.im, x1 * t.re)};
+        }
+        dft<R, M, false>(v, w);
+        cplx *dst = X + r * M;
+#pragma unroll
+        for (int kk = 0; kk < R; kk++) dst[u + kk * TPJ] = (u * kk) ? cmul(v[kk], w[u * kk]) : v[kk];
+    }
+    __syncthreads();
+    // ---- forward passes 1..P-1 ----
+    int L = TPJ / R;
+#pragma unroll
+    for (int s = 1; s < P; s++, L /= R) {
+        for (int jt = tid; jt < rows * TPJ; jt += blockDim.x) {
+            const int r = jt / TPJ, t = jt - r * TPJ;
+            const int g = t / L, u = t - g * L;
+            cplx *base = X + r * M + g * R * L + u;
+            cplx v[R];
+#pragma unroll
+            for (int m = 0; m < R; m++) v[m] = base[m * L];
+            dft<R, M, false>(v, w);
+            const int step = M / (R * L);
+#pragma unroll
+            for (int kk = 0; kk < R; kk++) base[kk * L] = (u * kk) ? cmul(v[kk], w[u * kk * step]) : v[kk];
+        }
+        __syncthreads();
+    }
+    // ---- pointwise multiply-accumulate with the GGSW (fixed fma order) ----
+    for (int idx = tid; idx < (k + 1) * M; idx += blockDim.x) {
+        const int c = idx / M, f = idx - c * M;
+        double re = 0.0, im = 0.0;
+        for (int lev = levels; lev >= 1; lev--)
+            for (int p = 0; p <= k; p++) {
+                const int r = (lev - 1) * (k + 1) + p;
+                const cplx x = X[r * M + f];
+                const cplx g = ggsw[((size_t)r * (k + 1) + c) * M + f];
+                re = fma(x.re, g.re, re);
+                re = fma(-x.im, g.im, re);
+                im = fma(x.re, g.im, im);
+                im = fma(x.im, g.re, im);
+            }
+        Y[c * M + f] = {re, im};
+    }
+    __syncthreads();
+    // ---- inverse passes P-1..1 (DIT) ----
+    L = 1;
+#pragma unroll
+    for (int s = P - 1; s >= 1; s--, L *= R) {
+        for (int jt = tid; jt < (k + 1) * TPJ; jt += blockDim.x) {
+            const int c = jt / TPJ, t = jt - c * TPJ;
+            const int g = t / L, u = t - g * L;
+            cplx *base = Y + c * M + g * R * L + u;
+            const int step = M / (R * L);
+            cplx v[R];
+#pragma unroll
+            for (int kk = 0; kk < R; kk++) v[kk] = (u * kk) ? cmul(base[kk * L], cconj(w[u * kk * step])) : base[kk * L];
+            dft<R, M, true>(v, w);
+#pragma unroll
+            for (int m = 0; m < R; m++) base[m * L] = v[m];
+        }
+        __syncthreads();
+    }
+    // ---- inverse pass 0 + untwist + torus rounding, accumulated into acc ----
+    for (int jt = tid; jt < (k + 1) * TPJ; jt += blockDim.x) {
+        const int c = jt / TPJ, u = jt - c * TPJ;
+        const cplx *base = Y + c * M + u;
+        cplx v[R];
+#pragma unroll
+        for (int kk = 0; kk < R; kk++) v[kk] = (u * kk) ? cmul(base[kk * TPJ], cconj(w[u * kk])) : base[kk * TPJ];
+        dft<R, M, true>(v, w);
+        uint64_t *out = acc + c * N;
+#pragma unroll
+        for (int m = 0; m < R; m++) {
+            const int j = u + m * TPJ;
+            const cplx t = cmul(v[m], untwist[j]);
+            out[j] += from_torus(t.re);
+            out[j + M] += from_torus(t.im);
+        }
+    }
+    __syncthreads();
+}
+
+template <int N>
+__device__ void sample_extract_store(const uint64_t *acc, int k, uint64_t body_add, uint64_t *out) {
+    for (int t = threadIdx.x; t < k * N; t += blockDim.x) {
+        const int p = t / N, j = t - p * N;
+        out[t] = j == 0 ? acc[p * N] : (0 - acc[p * N + N - j]);
+    }
+    if (threadIdx.x == 0) out[k * N] = acc[k * N] + body_add;
+}
+
+// ---------------------------------------------------------------------------------------------
+// PBS: one workgroup per ciphertext; ACC = LUT * X^{-b~}; for i < n with a_i != 0:
+// cmux(ACC, ACC * X^{a~_i}, BSK_i); extract coefficient 0.  (fft64 bootstrap.rs blind_rotate_assign)
+// ---------------------------------------------------------------------------------------------
+template <int N>
+__global__ void __launch_bounds__(kThreads) pbs_kernel(const uint64_t *__restrict__ lwe_in, uint64_t *__restrict__ lwe_out,
+                                                    const uint64_t *__restrict__ lut, const cplx *__restrict__ bsk,
+                                                    const cplx *__restrict__ twist, const cplx *__restrict__ untwist,
+                                                    const cplx *__restrict__ w, int n, int k, int levels, int base_log,
+                                                    uint64_t body_add, uint64_t out_add) {
+    constexpr int M = N / 2;
+    constexpr int logN = (N == 512) ? 9 : 10;
+    extern __shared__ __align__(16) unsigned char smem[];
+    uint64_t *acc = reinterpret_cast<uint64_t *>(smem);
+    cplx *X = reinterpret_cast<cplx *>(acc + (k + 1) * N);
+    cplx *Y = X + (k + 1) * levels * M;
+    const uint64_t *in = lwe_in + (size_t)blockIdx.x * (n + 1);
+    const int bt = mod_switch(in[n] + body_add, logN);
+    const int e0 = (2 * N - (bt % (2 * N))) % (2 * N);  // X^{-b~}
+    for (int t = threadIdx.x; t < (k + 1) * N; t += blockDim.x) {
+        const int c = t / N, j = t - c * N;
+        acc[t] = rotated_coeff(lut + c * N, j, e0, N);
+    }
+    __syncthreads();
+    const size_t ggsw_sz = (size_t)levels * (k + 1) * (k + 1) * M;
+    for (int i = 0; i < n; i++) {
+        const uint64_t a = in[i];
+        if (a == 0) continue;
+        const int e = mod_switch(a, logN) % (2 * N);
+        ext_product_step<N>(acc, X, Y, e, bsk + (size_t)i * ggsw_sz, k, levels, base_log, twist, untwist, w);
+    }
+    sample_extract_store<N>(acc, k, out_add, lwe_out + (size_t)blockIdx.x * (k * N + 1));
+}
+
+// ---------------------------------------------------------------------------------------------
+// Vertical packing (no CMux tree): workgroup (group g, output j): ACC = trivial(LUT_j); for the
+// GGSWs in reverse order, cmux(ACC, ACC * X^{-2^t}, GGSW); extract coefficient 0.
+// (wop_pbs::vertical_packing -> blind_rotate_assign)
+// ---------------------------------------------------------------------------------------------
+template <int N>
+__global__ void __launch_bounds__(kThreads) vp_kernel(const cplx *__restrict__ ggsw_f, int n_in, const uint64_t *__restrict__ lut,
+                                                   int n_out, uint64_t *__restrict__ out, const cplx *__restrict__ twist,
+                                                   const cplx *__restrict__ untwist, const cplx *__restrict__ w, int k,
+                                                   int levels, int base_log) {
+    constexpr int M = N / 2;
+    extern __shared__ __align__(16) unsigned char smem[];
+    uint64_t *acc = reinterpret_cast<uint64_t *>(smem);
+    cplx *X = reinterpret_cast<cplx *>(acc + (k + 1) * N);
+    cplx *Y = X + (k + 1) * levels * M;
+    const int g = blockIdx.x / n_out, jout = blockIdx.x - g * n_out;
+    for (int t = threadIdx.x; t < (k + 1) * N; t += blockDim.x) acc[t] = t < k * N ? 0 : lut[(size_t)jout * N + (t - k * N)];
+    __syncthreads();
+    const size_t ggsw_sz = (size_t)levels * (k + 1) * (k + 1) * M;
+    int deg = 1;
+    for (int b = n_in - 1; b >= 0; b--, deg <<= 1) {
+        const int e = 2 * N - deg;
+        ext_product_step<N>(acc, X, Y, e, ggsw_f + ((size_t)g * n_in + b) * ggsw_sz, k, levels, base_log, twist,
+                            untwist, w);
+    }
+    sample_extract_store<N>(acc, k, 0, out + ((size_t)g * n_out + jout) * (k * N + 1));
+}
+
+// ---------------------------------------------------------------------------------------------
+// Forward torus FFT of many polynomials (GGSW / BSK to the Fourier domain).  TPJ threads per
+// polynomial, 256/TPJ polynomials per workgroup.
+// ---------------------------------------------------------------------------------------------
+template <int N>
+__global__ void __launch_bounds__(kThreads) fft_torus_kernel(const uint64_t *__restrict__ in, cplx *__restrict__ out,
+                                                          size_t count, const cplx *__restrict__ twist,
+                                                          const cplx *__restrict__ w) {
+    constexpr int M = N / 2;
+    constexpr int R = FftPlan<M>::R, P = FftPlan<M>::P, TPJ = M / R, JPB = kThreads / TPJ;
+    extern __shared__ __align__(16) unsigned char smem[];
+    cplx *buf = reinterpret_cast<cplx *>(smem);
+    const int local = threadIdx.x / TPJ, u = threadIdx.x - local * TPJ;
+    const size_t poly = (size_t)blockIdx.x * JPB + local;
+    const bool active = poly < count;
+    cplx *X = buf + local * M;
+    if (active) {
+        const uint64_t *src = in + poly * N;
+        cplx v[R];
+#pragma unroll
+        for (int m = 0; m < R; m++) {
+            const int j = u + m * TPJ;
+            const double x0 = (double)(int64_t)src[j] * 0x1p-64, x1 = (double)(int64_t)src[j + M] * 0x1p-64;
+            const cplx t = twist[j];
+            v[m] = {fma(x0, t.re, -(x1 * t.im)), fma(x0, t.im, x1 * t.re)};
+        }
+        dft<R, M, false>(v, w);
+#pragma unroll
+        for (int kk = 0; kk < R; kk++) X[u + kk * TPJ] = (u * kk) ? cmul(v[kk], w[u * kk]) : v[kk];
+    }
+    __syncthreads();
+    int L = TPJ / R;
+#pragma unroll
+    for (int s = 1; s < P; s++, L /= R) {
+        if (active) {
+            const int gg = u / L, uu = u - gg * L;
+            cplx *base = X + gg * R * L + uu;
+            cplx v[R];
+#pragma unroll
+            for (int m = 0; m < R; m++) v[m] = base[m * L];
+            dft<R, M, false>(v, w);
+            const int step = M / (R * L);
+#pragma unroll
+            for (int kk = 0; kk < R; kk++) base[kk * L] = (uu * kk) ? cmul(v[kk], w[uu * kk * step]) : v[kk];
+        }
+        __syncthreads();
+    }
+    if (active) {
+        cplx *dst = out + poly * M;
+        for (int f = u; f < M; f += TPJ) dst[f] = X[f];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Keyswitch: out[b] = (0, .., 0, body) - sum_i sum_l d_{b,i,l} * KSK[i][l].  Thread = output
+// coefficient j, CT ciphertexts per workgroup; digits staged in LDS per chunk of inputs.
+// ---------------------------------------------------------------------------------------------
+constexpr int KS_CT = 16, KS_CHUNK = 64;
+
+__global__ void __launch_bounds__(kThreads) keyswitch_kernel(const uint64_t *__restrict__ in, uint64_t *__restrict__ out,
+                                                          const uint64_t *__restrict__ ksk, size_t B, int K, int n,
+                                                          int ks_l, int ks_b) {
+    __shared__ int8_t dig[KS_CT][KS_CHUNK][8];
+    const int j = blockIdx.x * kThreads + threadIdx.x;
+    const size_t b0 = (size_t)blockIdx.y * KS_CT;
+    uint64_t acc[KS_CT];
+#pragma unroll
+    for (int c = 0; c < KS_CT; c++) acc[c] = 0;
+    for (int i0 = 0; i0 < K; i0 += KS_CHUNK) {
+        for (int idx = threadIdx.x; idx < KS_CT * KS_CHUNK; idx += kThreads) {
+            const int c = idx / KS_CHUNK, ii = idx - c * KS_CHUNK;
+            const int i = i0 + ii;
+            const bool ok = (b0 + c < B) && i < K;
+            const uint64_t x = ok ? in[(b0 + c) * (K + 1) + i] : 0;
+            for (int l = 1; l <= ks_l; l++) dig[c][ii][l - 1] = ok ? (int8_t)decomp_digit(x, ks_b, ks_l, l) : 0;
+        }
+        __syncthreads();
+        if (j <= n) {
+            const int iend = min(KS_CHUNK, K - i0);
+            for (int ii = 0; ii < iend; ii++)
+                for (int l = 0; l < ks_l; l++) {
+                    const uint64_t key = ksk[((size_t)(i0 + ii) * ks_l + l) * (n + 1) + j];
+#pragma unroll
+                    for (int c = 0; c < KS_CT; c++) acc[c] -= mul_i32_u64(dig[c][ii][l], key);
+                }
+        }
+        __syncthreads();
+    }
+    if (j <= n)
+        for (int c = 0; c < KS_CT; c++)
+            if (b0 + c < B) out[(b0 + c) * (n + 1) + j] = acc[c] + (j == n ? in[(b0 + c) * (K + 1) + K] : 0);
+}
+
+// ---------------------------------------------------------------------------------------------
+// PFKS: GGSW row q of ciphertext b = - sum_{i<=K} sum_l d_{b,i,l} * PFPKSK[q][i][l]
+// ---------------------------------------------------------------------------------------------
+constexpr int PF_CT = 32, PF_CHUNK = 32;
+
+__global__ void __launch_bounds__(kThreads) pfks_kernel(const uint64_t *__restrict__ in, uint64_t *__restrict__ ggsw,
+                                                     const uint64_t *__restrict__ pfpksk, size_t B, int K, int glwe,
+                                                     int pf_l, int pf_b, int cbs_l, int level, int k) {
+    __shared__ int32_t dig[PF_CT][PF_CHUNK][4];
+    const int col = blockIdx.x * kThreads + threadIdx.x;
+    const int q = blockIdx.y;
+    const size_t b0 = (size_t)blockIdx.z * PF_CT;
+    uint64_t acc[PF_CT];
+#pragma unroll
+    for (int c = 0; c < PF_CT; c++) acc[c] = 0;
+    const uint64_t *key = pfpksk + (size_t)q * (K + 1) * pf_l * glwe;
+    for (int i0 = 0; i0 <= K; i0 += PF_CHUNK) {
+        for (int idx = threadIdx.x; idx < PF_CT * PF_CHUNK; idx += kThreads) {
+            const int c = idx / PF_CHUNK, ii = idx - c * PF_CHUNK;
+            const int i = i0 + ii;
+            const bool ok = (b0 + c < B) && i <= K;
+            const uint64_t x = ok ? in[(b0 + c) * (K + 1) + i] : 0;
+            for (int l = 1; l <= pf_l; l++) dig[c][ii][l - 1] = ok ? (int32_t)decomp_digit(x, pf_b, pf_l, l) : 0;
+        }
+        __syncthreads();
+        if (col < glwe) {
+            const int iend = min(PF_CHUNK, K + 1 - i0);
+            for (int ii = 0; ii < iend; ii++)
+                for (int l = 0; l < pf_l; l++) {
+                    const uint64_t kv = key[((size_t)(i0 + ii) * pf_l + l) * glwe + col];
+#pragma unroll
+                    for (int c = 0; c < PF_CT; c++) acc[c] -= mul_i32_u64(dig[c][ii][l], kv);
+                }
+        }
+        __syncthreads();
+    }
+    if (col < glwe)
+        for (int c = 0; c < PF_CT; c++)
+            if (b0 + c < B) ggsw[(((b0 + c) * cbs_l + (level - 1)) * (k + 1) + q) * (size_t)glwe + col] = acc[c];
+}
+
+// ---------------------------------------------------------------------------------------------
+// AES linear layer as LWE additions (state = [blk][16 bytes][8 bits][K+1])
+// ---------------------------------------------------------------------------------------------
+// state = blocks + rk[round 0]   (xor_state, data_model.rs:270-274)
+__global__ void aes_ark0_kernel(const uint64_t *__restrict__ blocks, const uint64_t *__restrict__ rk,
+                                uint64_t *__restrict__ state, size_t nb, int L) {
+    const size_t total = nb * 128 * (size_t)L;
+    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
+        const size_t within = t % (128 * (size_t)L);
+        state[t] = blocks[t] + rk[within];
+    }
+}
+
+// ShiftRows on the three SubBytes*{1,2,3} states, MixColumns, AddRoundKey:
+// out[r][c] = 2s[r][c'] + s[r+3][.] + s[r+2][.] + 3s[r+1][.]  (fhe_sbox_gal_mul_pbs.rs:61-82)
+__global__ void aes_mix_kernel(const uint64_t *__restrict__ muls, const uint64_t *__restrict__ rk_round,
+                               uint64_t *__restrict__ state, size_t nb, int L) {
+    const size_t total = nb * 128 * (size_t)L;
+    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
+        const size_t coef = t % L;
+        const size_t ct = t / L;  // blk*128 + pos*8 + bit
+        const int bit = (int)(ct & 7);
+        const int pos = (int)((ct >> 3) & 15);
+        const size_t blk = ct >> 7;
+        const int c = pos >> 2, row = pos & 3;
+        // after ShiftRows, element (rr, c) comes from SubBytes output byte 4*((c+rr)%4) + rr
+        auto src = [&](int rr, int m) {
+            const int byte = 4 * ((c + rr) & 3) + rr;
+            return muls[(((blk * 16 + byte) * 24) + 8 * m + bit) * (size_t)L + coef];
+        };
+        state[t] = src(row, 1) + src((row + 3) & 3, 0) + src((row + 2) & 3, 0) + src((row + 1) & 3, 2) +
+                   rk_round[(size_t)(pos * 8 + bit) * L + coef];
+    }
+}
+
+// last round: SubBytes (8->8), ShiftRows, AddRoundKey(rk[40..44])
+__global__ void aes_final_kernel(const uint64_t *__restrict__ sb, const uint64_t *__restrict__ rk_round,
+                                 uint64_t *__restrict__ out, size_t nb, int L) {
+    const size_t total = nb * 128 * (size_t)L;
+    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
+        const size_t coef = t % L;
+        const size_t ct = t / L;
+        const int bit = (int)(ct & 7);
+        const int pos = (int)((ct >> 3) & 15);
+        const size_t blk = ct >> 7;
+        const int c = pos >> 2, row = pos & 3;
+        const int byte = 4 * ((c + row) & 3) + row;
+        out[t] = sb[((blk * 16 + byte) * 8 + bit) * (size_t)L + coef] + rk_round[(size_t)(pos * 8 + bit) * L + coef];
+    }
+}
+
+__global__ void lwe_add_kernel(uint64_t *__restrict__ a, const uint64_t *__restrict__ b, size_t count) {
+    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < count; t += (size_t)gridDim.x * blockDim.x)
+        a[t] += b[t];
+}
+
+unsigned grid_for(size_t total) { return (unsigned)std::min<size_t>((total + kThreads - 1) / kThreads, 65536); }
+
+template <int N>
+size_t br_lds_bytes(int k, int levels) {
+    return (size_t)(k + 1) * N * 8 + (size_t)(k + 1) * levels * (N / 2) * 16 + (size_t)(k + 1) * (N / 2) * 16;
+}
+
+}  // namespace
+
+// =============================================================================================
+// Engine
+// =============================================================================================
+
+void *Engine::alloc(size_t bytes) {
+    void *p = nullptr;
+    HIPC(hipMalloc(&p, std::max<size_t>(bytes, 16)));
+    return p;
+}
+
+template <class T>
+T *Engine::grow(T *&ptr, size_t &cap, size_t count) {
+    if (count > cap) {
+        if (ptr) HIPC(hipFree(ptr));
+        ptr = static_cast<T *>(alloc(count * sizeof(T)));
+        cap = count;
+    }
+    return ptr;
+}
+
+void Engine::init_common() {
+    HIPC(hipSetDevice(device_));
+    HIPC(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    for (auto &e : ev_) HIPC(hipEventCreate(&e));
+    if (p_.N != 512 && p_.N != 1024) throw std::runtime_error("unsupported polynomial size");
+    const FftTables t = make_fft_tables(p_.N);
+    const size_t tb = sizeof(double) * 2 * t.M;
+    d_twist_ = static_cast<cplx *>(alloc(tb));
+    d_untwist_ = static_cast<cplx *>(alloc(tb));
+    d_w_ = static_cast<cplx *>(alloc(tb));
+    HIPC(hipMemcpy(d_twist_, t.twist.data(), tb, hipMemcpyHostToDevice));
+    HIPC(hipMemcpy(d_untwist_, t.untwist.data(), tb, hipMemcpyHostToDevice));
+    HIPC(hipMemcpy(d_w_, t.w.data(), tb, hipMemcpyHostToDevice));
+    // homomorphic_shift_boolean accumulators: body = -alpha, alpha = 2^(63 - cbs_b * level)
+    std::vector<uint64_t> luts((size_t)p_.cbs_l * p_.glwe_len(), 0);
+    for (int lev = 1; lev <= p_.cbs_l; lev++) {
+        const uint64_t alpha = 1ull << (63 - p_.cbs_b * lev);
+        for (int j = 0; j < p_.N; j++) luts[(size_t)(lev - 1) * p_.glwe_len() + (size_t)p_.k * p_.N + j] = 0 - alpha;
+    }
+    d_lut_shift_ = static_cast<uint64_t *>(alloc(luts.size() * 8));
+    HIPC(hipMemcpy(d_lut_shift_, luts.data(), luts.size() * 8, hipMemcpyHostToDevice));
+    // AES LUTs (fhe_impls/shortint_woppbs_1bit.rs:32-45, :94-128) -- built host-side once
+    std::vector<uint64_t> f24(256), f8(256);
+    for (int x = 0; x < 256; x++) {
+        const uint8_t s = kSbox[x];
+        f24[x] = ((uint64_t)gf_256_mul(s, 1) << 16) | ((uint64_t)gf_256_mul(s, 2) << 8) | gf_256_mul(s, 3);
+        f8[x] = s;
+    }
+    std::vector<uint64_t> l24(24 * lut_small_len(p_.N, 8)), l8(8 * lut_small_len(p_.N, 8));
+    generate_lut(p_.N, 8, 24, f24.data(), l24.data());
+    generate_lut(p_.N, 8, 8, f8.data(), l8.data());
+    d_lut24_ = static_cast<uint64_t *>(alloc(l24.size() * 8));
+    d_lut8_ = static_cast<uint64_t *>(alloc(l8.size() * 8));
+    HIPC(hipMemcpy(d_lut24_, l24.data(), l24.size() * 8, hipMemcpyHostToDevice));
+    HIPC(hipMemcpy(d_lut8_, l8.data(), l8.size() * 8, hipMemcpyHostToDevice));
+    // opt-in to >64 KiB dynamic LDS for the blind-rotation kernels
+    if (p_.N == 512) {
+        HIPC(hipFuncSetAttribute((const void *)pbs_kernel<512>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        HIPC(hipFuncSetAttribute((const void *)vp_kernel<512>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    } else {
+        HIPC(hipFuncSetAttribute((const void *)pbs_kernel<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        HIPC(hipFuncSetAttribute((const void *)vp_kernel<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    }
+}
+
+void Engine::bsk_to_fourier(const uint64_t *d_bsk_std) {
+    d_bsk_f_ = static_cast<cplx *>(alloc(p_.bsk_fourier_len() * sizeof(cplx)));
+    const size_t polys = (size_t)p_.n * p_.pbs_l * (p_.k + 1) * (p_.k + 1);
+    const int M = p_.M();
+    if (p_.N == 512) {
+        constexpr int JPB = kThreads / (256 / 16);
+        fft_torus_kernel<512><<<(unsigned)((polys + JPB - 1) / JPB), kThreads, JPB * M * sizeof(cplx), stream_>>>(
+            d_bsk_std, d_bsk_f_, polys, d_twist_, d_w_);
+    } else {
+        constexpr int JPB = kThreads / (512 / 8);
+        fft_torus_kernel<1024><<<(unsigned)((polys + JPB - 1) / JPB), kThreads, JPB * M * sizeof(cplx), stream_>>>(
+            d_bsk_std, d_bsk_f_, polys, d_twist_, d_w_);
+    }
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(stream_));
+}
+
+Engine::Engine(const ServerKeyRaw &keys, int device) : p_(keys.p), device_(device) {
+    init_common();
+    owns_keys_ = true;
+    d_ksk_ = static_cast<uint64_t *>(alloc(keys.ksk.size() * 8));
+    d_pfpksk_ = static_cast<uint64_t *>(alloc(keys.pfpksk.size() * 8));
+    HIPC(hipMemcpy(d_ksk_, keys.ksk.data(), keys.ksk.size() * 8, hipMemcpyHostToDevice));
+    HIPC(hipMemcpy(d_pfpksk_, keys.pfpksk.data(), keys.pfpksk.size() * 8, hipMemcpyHostToDevice));
+    uint64_t *d_bsk = static_cast<uint64_t *>(alloc(keys.bsk.size() * 8));
+    HIPC(hipMemcpy(d_bsk, keys.bsk.data(), keys.bsk.size() * 8, hipMemcpyHostToDevice));
+    bsk_to_fourier(d_bsk);
+    HIPC(hipFree(d_bsk));
+}
+
+Engine::Engine(const Params &p, int device, const uint64_t *d_ksk, const uint64_t *d_bsk,
+               const uint64_t *d_pfpksk)
+    : p_(p), device_(device) {
+    init_common();
+    owns_keys_ = false;
+    d_ksk_ = const_cast<uint64_t *>(d_ksk);
+    d_pfpksk_ = const_cast<uint64_t *>(d_pfpksk);
+    bsk_to_fourier(d_bsk);
+}
+
+Engine::~Engine() {
+    hipSetDevice(device_);
+    hipStreamSynchronize(stream_);
+    if (owns_keys_) {
+        hipFree(d_ksk_);
+        hipFree(d_pfpksk_);
+    }
+    for (void *q : {(void *)d_bsk_f_, (void *)d_twist_, (void *)d_untwist_, (void *)d_w_, (void *)d_lut_shift_,
+                    (void *)d_lut24_, (void *)d_lut8_, (void *)d_small_, (void *)d_big_, (void *)d_ggsw_,
+                    (void *)d_ggsw_f_, (void *)d_state_, (void *)d_muls_})
+        if (q) hipFree(q);
+    for (auto &e : ev_) hipEventDestroy(e);
+    hipStreamDestroy(stream_);
+}
+
+void Engine::synchronize() { HIPC(hipStreamSynchronize(stream_)); }
+
+void Engine::reserve(size_t bits, size_t outputs) {
+    grow(d_small_, cap_small_, bits * p_.small_len());
+    grow(d_big_, cap_big_, bits * p_.big_len());
+    grow(d_ggsw_, cap_ggsw_, bits * p_.cbs_ggsw_len());
+    grow(d_ggsw_f_, cap_ggsw_f_, bits * p_.cbs_ggsw_fourier_len());
+    (void)outputs;
+}
+
+void Engine::keyswitch(const uint64_t *d_in, uint64_t *d_out, size_t B) {
+    if (!B) return;
+    dim3 grid((unsigned)((p_.n + 1 + kThreads - 1) / kThreads), (unsigned)((B + KS_CT - 1) / KS_CT));
+    keyswitch_kernel<<<grid, kThreads, 0, stream_>>>(d_in, d_out, d_ksk_, B, p_.K(), p_.n, p_.ks_l, p_.ks_b);
+    HIPC(hipGetLastError());
+}
+
+void Engine::bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint64_t *d_big, size_t B,
+                       uint64_t body_add, uint64_t out_add) {
+    if (!B) return;
+    for (size_t off = 0; off < B; off += 65535) {
+        const unsigned g = (unsigned)std::min<size_t>(65535, B - off);
+        if (p_.N == 512) {
+            pbs_kernel<512><<<g, kThreads, br_lds_bytes<512>(p_.k, p_.pbs_l), stream_>>>(
+                d_small + off * p_.small_len(), d_big + off * p_.big_len(), d_lut_glwe, d_bsk_f_, d_twist_, d_untwist_,
+                d_w_, p_.n, p_.k, p_.pbs_l, p_.pbs_b, body_add, out_add);
+        } else {
+            pbs_kernel<1024><<<g, kThreads, br_lds_bytes<1024>(p_.k, p_.pbs_l), stream_>>>(
+                d_small + off * p_.small_len(), d_big + off * p_.big_len(), d_lut_glwe, d_bsk_f_, d_twist_, d_untwist_,
+                d_w_, p_.n, p_.k, p_.pbs_l, p_.pbs_b, body_add, out_add);
+        }
+        HIPC(hipGetLastError());
+    }
+}
+
+void Engine::pbs_shift_boolean(const uint64_t *d_small, uint64_t *d_big, size_t B, int level) {
+    const uint64_t alpha = 1ull << (63 - p_.cbs_b * level);
+    bootstrap(d_small, d_lut_shift_ + (size_t)(level - 1) * p_.glwe_len(), d_big, B, 1ull << 62, alpha);
+}
+
+void Engine::pfks_into_ggsw(const uint64_t *d_big, uint64_t *d_ggsw, size_t B, int level) {
+    if (!B) return;
+    const int glwe = (int)p_.glwe_len();
+    dim3 grid((unsigned)((glwe + kThreads - 1) / kThreads), (unsigned)(p_.k + 1), (unsigned)((B + PF_CT - 1) / PF_CT));
+    pfks_kernel<<<grid, kThreads, 0, stream_>>>(d_big, d_ggsw, d_pfpksk_, B, p_.K(), glwe, p_.pfks_l, p_.pfks_b,
+                                                p_.cbs_l, level, p_.k);
+    HIPC(hipGetLastError());
+}
+
+void Engine::ggsw_to_fourier(const uint64_t *d_ggsw, cplx *d_ggsw_f, size_t B) {
+    if (!B) return;
+    const size_t polys = B * p_.cbs_l * (p_.k + 1) * (p_.k + 1);
+    const int M = p_.M();
+    if (p_.N == 512) {
+        constexpr int JPB = kThreads / 16;
+        fft_torus_kernel<512><<<(unsigned)((polys + JPB - 1) / JPB), kThreads, JPB * M * sizeof(cplx), stream_>>>(
+            d_ggsw, d_ggsw_f, polys, d_twist_, d_w_);
+    } else {
+        constexpr int JPB = kThreads / 64;
+        fft_torus_kernel<1024><<<(unsigned)((polys + JPB - 1) / JPB), kThreads, JPB * M * sizeof(cplx), stream_>>>(
+            d_ggsw, d_ggsw_f, polys, d_twist_, d_w_);
+    }
+    HIPC(hipGetLastError());
+}
+
+void Engine::vertical_packing(const cplx *d_ggsw_f, size_t G, int n_in, const uint64_t *d_lut, int n_out,
+                              uint64_t *d_out) {
+    if (!G) return;
+    int logN = 0;
+    while ((1 << logN) < p_.N) logN++;
+    if (n_in > logN) throw std::runtime_error("vertical packing with a CMux tree (input_bits > log2 N) is not supported on device");
+    const size_t total = G * (size_t)n_out;
+    for (size_t off = 0; off < total; off += 65535 - (65535 % n_out)) {
+        const size_t chunk = std::min<size_t>(65535 - (65535 % n_out), total - off);
+        const size_t g0 = off / n_out;
+        if (p_.N == 512)
+            vp_kernel<512><<<(unsigned)chunk, kThreads, br_lds_bytes<512>(p_.k, p_.cbs_l), stream_>>>(
+                d_ggsw_f + g0 * n_in * p_.cbs_ggsw_fourier_len(), n_in, d_lut, n_out, d_out + g0 * n_out * p_.big_len(),
+                d_twist_, d_untwist_, d_w_, p_.k, p_.cbs_l, p_.cbs_b);
+        else
+            vp_kernel<1024><<<(unsigned)chunk, kThreads, br_lds_bytes<1024>(p_.k, p_.cbs_l), stream_>>>(
+                d_ggsw_f + g0 * n_in * p_.cbs_ggsw_fourier_len(), n_in, d_lut, n_out, d_out + g0 * n_out * p_.big_len(),
+                d_twist_, d_untwist_, d_w_, p_.k, p_.cbs_l, p_.cbs_b);
+        HIPC(hipGetLastError());
+    }
+}
+
+void Engine::circuit_bootstrap(const uint64_t *d_bits, size_t G, int n_in, const uint64_t *d_lut, int n_out,
+                               uint64_t *d_out) {
+    const size_t bits = G * n_in;
+    reserve(bits, G * n_out);
+    if (timing_) HIPC(hipEventRecord(ev_[0], stream_));
+    keyswitch(d_bits, d_small_, bits);
+    if (timing_) HIPC(hipEventRecord(ev_[1], stream_));
+    for (int lev = 1; lev <= p_.cbs_l; lev++) {
+        pbs_shift_boolean(d_small_, d_big_, bits, lev);
+        if (timing_ && lev == p_.cbs_l) HIPC(hipEventRecord(ev_[2], stream_));
+        pfks_into_ggsw(d_big_, d_ggsw_, bits, lev);
+    }
+    if (timing_) HIPC(hipEventRecord(ev_[3], stream_));
+    ggsw_to_fourier(d_ggsw_, d_ggsw_f_, bits);
+    if (timing_) HIPC(hipEventRecord(ev_[4], stream_));
+    vertical_packing(d_ggsw_f_, G, n_in, d_lut, n_out, d_out);
+    if (timing_) {
+        HIPC(hipEventRecord(ev_[5], stream_));
+        HIPC(hipEventSynchronize(ev_[5]));
+        float ms;
+        HIPC(hipEventElapsedTime(&ms, ev_[0], ev_[1])); times_.keyswitch += ms;
+        HIPC(hipEventElapsedTime(&ms, ev_[1], ev_[2])); times_.pbs += ms;
+        HIPC(hipEventElapsedTime(&ms, ev_[2], ev_[3])); times_.pfks += ms;
+        HIPC(hipEventElapsedTime(&ms, ev_[3], ev_[4])); times_.ggsw_fft += ms;
+        HIPC(hipEventElapsedTime(&ms, ev_[4], ev_[5])); times_.vertical_packing += ms;
+        times_.pbs_launches += p_.cbs_l;
+    }
+}
+
+void Engine::aes_encrypt_blocks(const uint64_t *d_rk, const uint64_t *d_blocks, size_t nb, int rounds,
+                                uint64_t *d_out) {
+    if (!nb) return;
+    if (rounds < 1 || rounds > 10) throw std::runtime_error("rounds must be in 1..=10");
+    const int L = (int)p_.big_len();
+    const size_t state_len = nb * 128 * (size_t)L;
+    times_ = StageTimes{};
+    grow(d_state_, cap_state_, state_len);
+    grow(d_muls_, cap_muls_, nb * 16 * 24 * (size_t)L);
+    const size_t byte_stride = 8 * (size_t)L;
+    aes_ark0_kernel<<<grid_for(state_len), kThreads, 0, stream_>>>(d_blocks, d_rk, d_state_, nb, L);
+    HIPC(hipGetLastError());
+    for (int r = 1; r < rounds; r++) {
+        circuit_bootstrap(d_state_, nb * 16, 8, d_lut24_, 24, d_muls_);
+        aes_mix_kernel<<<grid_for(state_len), kThreads, 0, stream_>>>(d_muls_, d_rk + (size_t)16 * r * byte_stride,
+                                                                       d_state_, nb, L);
+        HIPC(hipGetLastError());
+    }
+    circuit_bootstrap(d_state_, nb * 16, 8, d_lut8_, 8, d_muls_);
+    aes_final_kernel<<<grid_for(state_len), kThreads, 0, stream_>>>(d_muls_, d_rk + (size_t)160 * byte_stride, d_out,
+                                                                     nb, L);
+    HIPC(hipGetLastError());
+}
+
+void Engine::lwe_add(uint64_t *d_a, const uint64_t *d_b, size_t count) {
+    lwe_add_kernel<<<grid_for(count), kThreads, 0, stream_>>>(d_a, d_b, count);
+    HIPC(hipGetLastError());
+}
+
+}  // namespace tae

@@ -1,0 +1,337 @@
+// Host-side model mirror: noise bookkeeping, circuit_bootstrap, AES round driver, key schedule.
+// See model.hpp for the reference mapping.
+#include "model.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+#include "aes.hpp"
+#include "cplx.hpp"
+#include "../../include/tfhe_aes_gpu.h"
+
+namespace tae {
+
+// ---------------------------------------------------------------------------------------------
+// AES constants (src/aes_128.rs)
+// ---------------------------------------------------------------------------------------------
+const uint8_t kSbox[256] = {
+    0x63, 0x7c, 0x77, 0x7b, 0xf2, 0x6b, 0x6f, 0xc5, 0x30, 0x01, 0x67, 0x2b, 0xfe, 0xd7, 0xab, 0x76, 0xca, 0x82,
+    0xc9, 0x7d, 0xfa, 0x59, 0x47, 0xf0, 0xad, 0xd4, 0xa2, 0xaf, 0x9c, 0xa4, 0x72, 0xc0, 0xb7, 0xfd, 0x93, 0x26,
+    0x36, 0x3f, 0xf7, 0xcc, 0x34, 0xa5, 0xe5, 0xf1, 0x71, 0xd8, 0x31, 0x15, 0x04, 0xc7, 0x23, 0xc3, 0x18, 0x96,
+    0x05, 0x9a, 0x07, 0x12, 0x80, 0xe2, 0xeb, 0x27, 0xb2, 0x75, 0x09, 0x83, 0x2c, 0x1a, 0x1b, 0x6e, 0x5a, 0xa0,
+    0x52, 0x3b, 0xd6, 0xb3, 0x29, 0xe3, 0x2f, 0x84, 0x53, 0xd1, 0x00, 0xed, 0x20, 0xfc, 0xb1, 0x5b, 0x6a, 0xcb,
+    0xbe, 0x39, 0x4a, 0x4c, 0x58, 0xcf, 0xd0, 0xef, 0xaa, 0xfb, 0x43, 0x4d, 0x33, 0x85, 0x45, 0xf9, 0x02, 0x7f,
+    0x50, 0x3c, 0x9f, 0xa8, 0x51, 0xa3, 0x40, 0x8f, 0x92, 0x9d, 0x38, 0xf5, 0xbc, 0xb6, 0xda, 0x21, 0x10, 0xff,
+    0xf3, 0xd2, 0xcd, 0x0c, 0x13, 0xec, 0x5f, 0x97, 0x44, 0x17, 0xc4, 0xa7, 0x7e, 0x3d, 0x64, 0x5d, 0x19, 0x73,
+    0x60, 0x81, 0x4f, 0xdc, 0x22, 0x2a, 0x90, 0x88, 0x46, 0xee, 0xb8, 0x14, 0xde, 0x5e, 0x0b, 0xdb, 0xe0, 0x32,
+    0x3a, 0x0a, 0x49, 0x06, 0x24, 0x5c, 0xc2, 0xd3, 0xac, 0x62, 0x91, 0x95, 0xe4, 0x79, 0xe7, 0xc8, 0x37, 0x6d,
+    0x8d, 0xd5, 0x4e, 0xa9, 0x6c, 0x56, 0xf4, 0xea, 0x65, 0x7a, 0xae, 0x08, 0xba, 0x78, 0x25, 0x2e, 0x1c, 0xa6,
+    0xb4, 0xc6, 0xe8, 0xdd, 0x74, 0x1f, 0x4b, 0xbd, 0x8b, 0x8a, 0x70, 0x3e, 0xb5, 0x66, 0x48, 0x03, 0xf6, 0x0e,
+    0x61, 0x35, 0x57, 0xb9, 0x86, 0xc1, 0x1d, 0x9e, 0xe1, 0xf8, 0x98, 0x11, 0x69, 0xd9, 0x8e, 0x94, 0x9b, 0x1e,
+    0x87, 0xe9, 0xce, 0x55, 0x28, 0xdf, 0x8c, 0xa1, 0x89, 0x0d, 0xbf, 0xe6, 0x42, 0x68, 0x41, 0x99, 0x2d, 0x0f,
+    0xb0, 0x54, 0xbb, 0x16};
+const uint8_t kRcon[11] = {0x00, 0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80, 0x1B, 0x36};
+
+uint8_t gf_256_mul(uint8_t a, uint8_t b) {
+    uint8_t res = 0;
+    for (int i = 0; i < 8; i++) {
+        if (b & 1) res ^= a;
+        const uint8_t high_bit = a & 0x80;
+        a = (uint8_t)(a << 1);
+        if (high_bit != 0x80) a ^= 0x1b;  // sic: aes_128.rs:50
+        b >>= 1;
+    }
+    return res;
+}
+
+void plain_key_schedule(const uint8_t key[16], uint8_t rk[176]) {
+    std::memcpy(rk, key, 16);
+    for (int i = 4; i < 44; i++) {
+        uint8_t t[4];
+        std::memcpy(t, rk + 4 * (i - 1), 4);
+        if (i % 4 == 0) {
+            const uint8_t first = t[0];
+            t[0] = (uint8_t)(kSbox[t[1]] ^ kRcon[i / 4]);
+            t[1] = kSbox[t[2]];
+            t[2] = kSbox[t[3]];
+            t[3] = kSbox[first];
+        }
+        for (int j = 0; j < 4; j++) rk[4 * i + j] = rk[4 * (i - 4) + j] ^ t[j];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Noise bookkeeping
+// ---------------------------------------------------------------------------------------------
+static std::atomic<uint64_t> g_ct_counter{0};
+uint64_t next_ct_id() { return g_ct_counter.fetch_add(1); }
+
+void NoiseLevel::add_assign(const NoiseLevel &rhs, uint64_t max_noise_sq) {
+    // assert!(components ∩ rhs.components == ∅, "noise components not independent")
+    auto a = components.cbegin();
+    auto b = rhs.components.cbegin();
+    while (a != components.cend() && b != rhs.components.cend()) {
+        if (*a == *b) throw ModelError{TAE_E_INDEP, "noise components not independent"};
+        if (*a < *b)
+            ++a;
+        else
+            ++b;
+    }
+    std::vector<uint64_t> merged;
+    merged.reserve(components.size() + rhs.components.size());
+    std::merge(components.begin(), components.end(), rhs.components.begin(), rhs.components.end(),
+               std::back_inserter(merged));
+    components.swap(merged);
+    noise_level_squared += rhs.noise_level_squared;
+    if (noise_level_squared > max_noise_sq)  // MaxNoiseLevel::validate(..).unwrap()
+        throw ModelError{TAE_E_NOISE, "NoiseTooBig { noise_level: " + std::to_string(noise_level_squared) +
+                                          ", max_noise_level: " + std::to_string(max_noise_sq) + " }"};
+}
+
+void BitCt::xor_assign(const BitCt &rhs) {
+    if (rhs.ct.size() != ct.size()) throw ModelError{TAE_E_ARG, "ciphertext size mismatch"};
+    for (size_t i = 0; i < ct.size(); i++) ct[i] += rhs.ct[i];  // lwe_ciphertext_add_assign
+    noise.add_assign(rhs.noise, max_noise_sq);
+}
+
+BitCt Context::trivial(uint64_t bit) const {
+    if (bit > 1) throw ModelError{TAE_E_ARG, "cleartext out of bounds: " + std::to_string(bit)};
+    BitCt b;
+    b.ct.assign(params().big_len(), 0);
+    b.ct.back() = encode_bit(bit);
+    b.noise = NoiseLevel::trivial();
+    b.max_noise_sq = params().max_noise_sq;
+    return b;
+}
+
+BitCt Context::wrap(std::vector<uint64_t> ct, uint64_t noise_level_squared) const {
+    BitCt b;
+    b.ct = std::move(ct);
+    b.noise = NoiseLevel::with_noise_level(noise_level_squared, next_ct_id());
+    b.max_noise_sq = params().max_noise_sq;
+    return b;
+}
+
+Lut Context::generate_lookup_table(int input_bits, int output_bits, const uint64_t *f_values) const {
+    if (!(input_bits > 0 && input_bits <= 16)) throw ModelError{TAE_E_PARAM, "input_bits must be in 1..=16"};
+    if (!(output_bits > 0 && output_bits <= 64)) throw ModelError{TAE_E_PARAM, "output_bits must be in 1..=64"};
+    Lut l;
+    l.input_bits = input_bits;
+    l.output_bits = output_bits;
+    l.small_len = lut_small_len(params().N, input_bits);
+    l.data.assign(l.small_len * output_bits, 0);
+    generate_lut(params().N, input_bits, output_bits, f_values, l.data.data());
+    return l;
+}
+
+namespace {
+struct DevBuf {
+    void *p = nullptr;
+    explicit DevBuf(size_t bytes) { hip_check(hipMalloc(&p, std::max<size_t>(bytes, 16)), "hipMalloc"); }
+    ~DevBuf() {
+        if (p) hipFree(p);
+    }
+    template <class T>
+    T *as() const {
+        return static_cast<T *>(p);
+    }
+};
+}  // namespace
+
+void Context::circuit_bootstrap_raw(const uint64_t *bits, size_t groups, int n_in, const Lut &lut, uint64_t *out,
+                                    bool device_mem) {
+    if (n_in != lut.input_bits) throw ModelError{TAE_E_ARG, "number of input bits does not match the LUT"};
+    if (lut.small_len != (size_t)params().N)
+        throw ModelError{TAE_E_PARAM, "LUTs with input_bits > log2(N) need the CMux tree (not on device yet)"};
+    std::lock_guard<std::mutex> g(mu_);
+    const size_t L = params().big_len();
+    hip_check(hipSetDevice(engine_->device()), "hipSetDevice");
+    DevBuf d_lut(lut.data.size() * 8);
+    hip_check(hipMemcpyAsync(d_lut.p, lut.data.data(), lut.data.size() * 8, hipMemcpyHostToDevice,
+                             engine_->stream()),
+              "lut upload");
+    if (device_mem) {
+        engine_->circuit_bootstrap(bits, groups, n_in, d_lut.as<uint64_t>(), lut.output_bits, out);
+        engine_->synchronize();
+        return;
+    }
+    DevBuf d_in(groups * n_in * L * 8), d_out(groups * lut.output_bits * L * 8);
+    hip_check(hipMemcpyAsync(d_in.p, bits, groups * n_in * L * 8, hipMemcpyHostToDevice, engine_->stream()), "upload");
+    engine_->circuit_bootstrap(d_in.as<uint64_t>(), groups, n_in, d_lut.as<uint64_t>(), lut.output_bits,
+                               d_out.as<uint64_t>());
+    hip_check(hipMemcpyAsync(out, d_out.p, groups * lut.output_bits * L * 8, hipMemcpyDeviceToHost, engine_->stream()),
+              "download");
+    engine_->synchronize();
+}
+
+// FheContext::circuit_bootstrap (shortint_woppbs_1bit.rs:292-336)
+std::vector<BitCt> Context::circuit_bootstrap(const std::vector<const BitCt *> &bits, const Lut &lut) {
+    const size_t L = params().big_len();
+    std::vector<uint64_t> in(bits.size() * L), out((size_t)lut.output_bits * L);
+    for (size_t b = 0; b < bits.size(); b++) std::memcpy(&in[b * L], bits[b]->ct.data(), L * 8);
+    circuit_bootstrap_raw(in.data(), 1, (int)bits.size(), lut, out.data(), false);
+    // Lemma 3.2 of eprint 2017/430: output noise^2 = NOMINAL * input_bit_count (:322-325)
+    std::vector<BitCt> res;
+    for (int j = 0; j < lut.output_bits; j++)
+        res.push_back(wrap(std::vector<uint64_t>(out.begin() + j * L, out.begin() + (j + 1) * L), bits.size()));
+    return res;
+}
+
+// ---------------------------------------------------------------------------------------------
+// AES (fhe_sbox_gal_mul_pbs.rs)
+// ---------------------------------------------------------------------------------------------
+// Metadata-only replay of encrypt_block_for_rounds for ONE block: rk [44*32], block [128].
+std::vector<NoiseLevel> aes_noise_schedule(const std::vector<NoiseLevel> &rk, const std::vector<NoiseLevel> &block,
+                                           int rounds, uint64_t max) {
+    auto key_bit = [&](int word, int byte, int bit) -> const NoiseLevel & { return rk[(word * 4 + byte) * 8 + bit]; };
+    std::vector<NoiseLevel> st = block;  // index (4*col + row)*8 + bit
+    for (int c = 0; c < 4; c++)
+        for (int r = 0; r < 4; r++)
+            for (int b = 0; b < 8; b++) st[(4 * c + r) * 8 + b].add_assign(key_bit(c, r, b), max);
+    auto cbs_outputs = [&](int n_out) {
+        std::vector<NoiseLevel> o((size_t)16 * n_out);
+        for (auto &x : o) x = NoiseLevel::with_noise_level(8, next_ct_id());
+        return o;
+    };
+    for (int round = 1; round < rounds; round++) {
+        std::vector<NoiseLevel> muls = cbs_outputs(24);  // [byte][24]
+        auto src = [&](int rr, int c, int m, int b) -> const NoiseLevel & {
+            return muls[(4 * ((c + rr) % 4) + rr) * 24 + 8 * m + b];
+        };
+        for (int c = 0; c < 4; c++)
+            for (int r = 0; r < 4; r++)
+                for (int b = 0; b < 8; b++) {
+                    NoiseLevel v = src(r, c, 1, b);
+                    v.add_assign(src((r + 3) % 4, c, 0, b), max);
+                    v.add_assign(src((r + 2) % 4, c, 0, b), max);
+                    v.add_assign(src((r + 1) % 4, c, 2, b), max);
+                    v.add_assign(key_bit(4 * round + c, r, b), max);
+                    st[(4 * c + r) * 8 + b] = std::move(v);
+                }
+    }
+    std::vector<NoiseLevel> sb = cbs_outputs(8);
+    for (int c = 0; c < 4; c++)
+        for (int r = 0; r < 4; r++)
+            for (int b = 0; b < 8; b++) {
+                NoiseLevel v = sb[(4 * ((c + r) % 4) + r) * 8 + b];
+                v.add_assign(key_bit(40 + c, r, b), max);
+                st[(4 * c + r) * 8 + b] = std::move(v);
+            }
+    return st;
+}
+
+void Context::aes_encrypt_blocks_raw(const uint64_t *rk, const uint64_t *blocks, size_t n_blocks, int rounds,
+                                     uint64_t *out, bool device_mem) {
+    if (rounds < 1 || rounds > kAesRounds) throw ModelError{TAE_E_PARAM, "rounds must be in 1..=10"};
+    {
+        // static validation of the fixed AES noise schedule for fresh inputs (noise^2 = 1)
+        std::vector<NoiseLevel> krk(44 * 32), kbl(128);
+        for (auto &x : krk) x = NoiseLevel::with_noise_level(1, next_ct_id());
+        for (auto &x : kbl) x = NoiseLevel::with_noise_level(1, next_ct_id());
+        aes_noise_schedule(krk, kbl, rounds, params().max_noise_sq);
+    }
+    std::lock_guard<std::mutex> g(mu_);
+    hip_check(hipSetDevice(engine_->device()), "hipSetDevice");
+    const size_t L = params().big_len();
+    if (device_mem) {
+        engine_->aes_encrypt_blocks(rk, blocks, n_blocks, rounds, out);
+        engine_->synchronize();
+        return;
+    }
+    DevBuf d_rk(44 * 32 * L * 8), d_in(n_blocks * 128 * L * 8), d_out(n_blocks * 128 * L * 8);
+    hip_check(hipMemcpyAsync(d_rk.p, rk, 44 * 32 * L * 8, hipMemcpyHostToDevice, engine_->stream()), "upload rk");
+    hip_check(hipMemcpyAsync(d_in.p, blocks, n_blocks * 128 * L * 8, hipMemcpyHostToDevice, engine_->stream()),
+              "upload blocks");
+    engine_->aes_encrypt_blocks(d_rk.as<uint64_t>(), d_in.as<uint64_t>(), n_blocks, rounds, d_out.as<uint64_t>());
+    hip_check(hipMemcpyAsync(out, d_out.p, n_blocks * 128 * L * 8, hipMemcpyDeviceToHost, engine_->stream()),
+              "download");
+    engine_->synchronize();
+}
+
+std::vector<BitCt> Context::aes_encrypt_blocks(const std::vector<const BitCt *> &expanded_key,
+                                               const std::vector<const BitCt *> &blocks, size_t n_blocks,
+                                               int rounds) {
+    if (expanded_key.size() != 44 * 32) throw ModelError{TAE_E_ARG, "expanded key must be 44 words (1408 bits)"};
+    if (blocks.size() != n_blocks * 128) throw ModelError{TAE_E_ARG, "blocks must be 128 bits each"};
+    if (rounds < 1 || rounds > kAesRounds) throw ModelError{TAE_E_PARAM, "rounds must be in 1..=10"};
+    const size_t L = params().big_len();
+    std::vector<NoiseLevel> krk(44 * 32);
+    for (size_t i = 0; i < krk.size(); i++) krk[i] = expanded_key[i]->noise;
+    std::vector<std::vector<NoiseLevel>> out_noise(n_blocks);
+    for (size_t blk = 0; blk < n_blocks; blk++) {
+        std::vector<NoiseLevel> kb(128);
+        for (int i = 0; i < 128; i++) kb[i] = blocks[blk * 128 + i]->noise;
+        out_noise[blk] = aes_noise_schedule(krk, kb, rounds, params().max_noise_sq);
+    }
+    std::vector<uint64_t> rk(44 * 32 * L), in(n_blocks * 128 * L), out(n_blocks * 128 * L);
+    for (size_t i = 0; i < 44 * 32; i++) std::memcpy(&rk[i * L], expanded_key[i]->ct.data(), L * 8);
+    for (size_t i = 0; i < n_blocks * 128; i++) std::memcpy(&in[i * L], blocks[i]->ct.data(), L * 8);
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        hip_check(hipSetDevice(engine_->device()), "hipSetDevice");
+        DevBuf d_rk(rk.size() * 8), d_in(in.size() * 8), d_out(out.size() * 8);
+        hip_check(hipMemcpyAsync(d_rk.p, rk.data(), rk.size() * 8, hipMemcpyHostToDevice, engine_->stream()), "up");
+        hip_check(hipMemcpyAsync(d_in.p, in.data(), in.size() * 8, hipMemcpyHostToDevice, engine_->stream()), "up");
+        engine_->aes_encrypt_blocks(d_rk.as<uint64_t>(), d_in.as<uint64_t>(), n_blocks, rounds, d_out.as<uint64_t>());
+        hip_check(hipMemcpyAsync(out.data(), d_out.p, out.size() * 8, hipMemcpyDeviceToHost, engine_->stream()), "dn");
+        engine_->synchronize();
+    }
+    std::vector<BitCt> res(n_blocks * 128);
+    for (size_t i = 0; i < n_blocks * 128; i++) {
+        res[i].ct.assign(out.begin() + i * L, out.begin() + (i + 1) * L);
+        res[i].noise = out_noise[i / 128][i % 128];
+        res[i].max_noise_sq = params().max_noise_sq;
+    }
+    return res;
+}
+
+// fhe_sbox_gal_mul_pbs::key_schedule (:134-164) with ByteT::{sbox_substitute, bootstrap_assign}
+// (fhe_impls/shortint_woppbs_1bit.rs:18-45): words 0..3 = key; word i>=4 from words i-4, i-1
+// (SubWord(RotWord) + Rcon when i%4 == 0), then every bit of word i is bootstrapped (identity LUT).
+std::vector<BitCt> Context::aes_key_schedule(const std::vector<const BitCt *> &key) {
+    if (key.size() != 128) throw ModelError{TAE_E_ARG, "key must be 16 bytes (128 bits)"};
+    const size_t L = params().big_len();
+    std::vector<BitCt> ek(44 * 32);
+    for (int i = 0; i < 128; i++) ek[i] = *key[i];
+    uint64_t ftab_sbox[256], ftab_id[2] = {0, 1};
+    for (int x = 0; x < 256; x++) ftab_sbox[x] = kSbox[x];
+    const Lut sbox = generate_lookup_table(8, 8, ftab_sbox);
+    const Lut ident = generate_lookup_table(1, 1, ftab_id);
+    auto bit_at = [&](int word, int byte, int bit) -> BitCt & { return ek[(word * 4 + byte) * 8 + bit]; };
+    std::vector<uint64_t> in, out;
+    for (int i = 4; i < 44; i++) {
+        std::vector<BitCt> w(32);
+        if (i % 4 == 0) {
+            // sub_word(rotate_left(ek[i-1], 1)): 4 SBOX circuit bootstraps (one batched call)
+            in.assign(4 * 8 * L, 0);
+            out.assign(4 * 8 * L, 0);
+            for (int byte = 0; byte < 4; byte++)
+                for (int b = 0; b < 8; b++)
+                    std::memcpy(&in[(byte * 8 + b) * L], bit_at(i - 1, (byte + 1) % 4, b).ct.data(), L * 8);
+            circuit_bootstrap_raw(in.data(), 4, 8, sbox, out.data(), false);
+            for (int t = 0; t < 32; t++) {
+                BitCt s = wrap(std::vector<uint64_t>(out.begin() + t * L, out.begin() + (t + 1) * L), 8);
+                BitCt v = ek[(i - 4) * 32 + t];
+                v.xor_assign(s);
+                w[t] = std::move(v);
+            }
+            for (int b = 0; b < 8; b++) w[b].xor_assign(trivial((kRcon[i / 4] >> (7 - b)) & 1));
+        } else {
+            for (int t = 0; t < 32; t++) {
+                BitCt v = ek[(i - 4) * 32 + t];
+                v.xor_assign(ek[(i - 1) * 32 + t]);
+                w[t] = std::move(v);
+            }
+        }
+        // boot_word: identity circuit bootstrap of every bit (32 one-bit groups, one call)
+        in.assign(32 * L, 0);
+        out.assign(32 * L, 0);
+        for (int t = 0; t < 32; t++) std::memcpy(&in[t * L], w[t].ct.data(), L * 8);
+        circuit_bootstrap_raw(in.data(), 32, 1, ident, out.data(), false);
+        for (int t = 0; t < 32; t++)
+            ek[i * 32 + t] = wrap(std::vector<uint64_t>(out.begin() + t * L, out.begin() + (t + 1) * L), 1);
+    }
+    return ek;
+}
+
+}  // namespace tae

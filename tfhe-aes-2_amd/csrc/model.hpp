@@ -1,0 +1,93 @@
+// Host-side mirror of the reference's model and AES traits, driving the device Engine.
+//
+// Reference (allanbrondum/tfhe-aes-2):
+//   src/tfhe.rs:11-24                       ClientKeyT / ContextT
+//   src/tfhe/shortint_woppbs_1bit.rs:26-151  BitCt, NoiseLevelWithComponents, BitXorAssign
+//   src/tfhe/shortint_woppbs_1bit.rs:165-336 FheContext (ct ids, generate_lookup_table,
+//                                            circuit_bootstrap)
+//   src/aes_128/fhe/fhe_impls/shortint_woppbs_1bit.rs:17-151
+//                                            ByteT impls + ShortintWoppbs1BitSboxGalMulPbsAesEncrypt
+//   src/aes_128/fhe/fhe_sbox_gal_mul_pbs.rs:27-191 encrypt_block_for_rounds, key_schedule
+// The ciphertext arithmetic runs in the Engine (HIP); this layer keeps the reference's noise
+// bookkeeping (noise^2 level + independent component ids) on the host, per ciphertext.
+#pragma once
+#include <atomic>
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "client.hpp"
+#include "engine.hpp"
+
+namespace tae {
+
+// Reference panics become status codes.
+struct ModelError {
+    int code;  // TAE_E_NOISE / TAE_E_INDEP / TAE_E_PARAM / TAE_E_ARG
+    std::string msg;
+};
+
+// NoiseLevelWithComponents (shortint_woppbs_1bit.rs:34-78)
+struct NoiseLevel {
+    uint64_t noise_level_squared = 0;
+    std::vector<uint64_t> components;  // sorted CiphertextIds
+
+    static NoiseLevel with_noise_level(uint64_t nl, uint64_t id) { return {nl, {id}}; }
+    static NoiseLevel trivial() { return {}; }
+    // add_assign: asserts disjoint components, unions them, adds noise^2 and validates <= max
+    void add_assign(const NoiseLevel &rhs, uint64_t max_noise_sq);
+};
+
+uint64_t next_ct_id();  // FheContext::next_ct_id (process-wide counter)
+
+struct BitCt {
+    std::vector<uint64_t> ct;  // [K+1]
+    NoiseLevel noise;
+    uint64_t max_noise_sq = 0;
+
+    void xor_assign(const BitCt &rhs);  // BitXorAssign
+};
+
+struct Lut {  // WopbsLUTBase
+    int input_bits = 0, output_bits = 0;
+    size_t small_len = 0;
+    std::vector<uint64_t> data;  // [output_bits][small_len]
+};
+
+class Context {  // FheContext
+  public:
+    Context(std::unique_ptr<Engine> engine) : engine_(std::move(engine)) {}
+    const Params &params() const { return engine_->params(); }
+    Engine &engine() { return *engine_; }
+    std::mutex &mutex() { return mu_; }
+
+    BitCt trivial(uint64_t bit) const;
+    BitCt wrap(std::vector<uint64_t> ct, uint64_t noise_level_squared) const;  // BitCt::with_noise_level
+    Lut generate_lookup_table(int input_bits, int output_bits, const uint64_t *f_values) const;
+    std::vector<BitCt> circuit_bootstrap(const std::vector<const BitCt *> &bits, const Lut &lut);
+    // batched raw circuit bootstrap (device or host arrays)
+    void circuit_bootstrap_raw(const uint64_t *bits, size_t groups, int n_in, const Lut &lut, uint64_t *out,
+                               bool device_mem);
+
+    // Aes128Encrypt::encrypt_block_for_rounds over many blocks (noise bookkeeping per bit)
+    std::vector<BitCt> aes_encrypt_blocks(const std::vector<const BitCt *> &expanded_key,
+                                          const std::vector<const BitCt *> &blocks, size_t n_blocks, int rounds);
+    // fhe_sbox_gal_mul_pbs::key_schedule
+    std::vector<BitCt> aes_key_schedule(const std::vector<const BitCt *> &key);
+    // raw arrays, fresh inputs; static noise-schedule validation
+    void aes_encrypt_blocks_raw(const uint64_t *rk, const uint64_t *blocks, size_t n_blocks, int rounds,
+                                uint64_t *out, bool device_mem);
+
+  private:
+    std::unique_ptr<Engine> engine_;
+    std::mutex mu_;
+};
+
+// Noise bookkeeping of the AES round function on metadata only: returns output noise levels
+// (per bit) or throws ModelError exactly where the reference would panic.
+std::vector<NoiseLevel> aes_noise_schedule(const std::vector<NoiseLevel> &rk, const std::vector<NoiseLevel> &block,
+                                           int rounds, uint64_t max_noise_sq);
+
+}  // namespace tae

@@ -1,0 +1,61 @@
+// Parameter sets of the 1-bit WoP-PBS model.
+// Reference: src/tfhe/shortint_woppbs_1bit/parameters.rs:29-205 (WopbsParameters +
+// max_noise_level_squared).  Default for the AES path: params_sqrd_lvl_64 (main.rs:82-83).
+#pragma once
+#include <cstddef>
+#include <cstdint>
+
+namespace tae {
+
+struct Params {
+    int id;
+    int n;  // lwe_dimension (small key)
+    int k;  // glwe_dimension
+    int N;  // polynomial_size
+    int pbs_l, pbs_b;
+    int ks_l, ks_b;
+    int cbs_l, cbs_b;
+    int pfks_l, pfks_b;
+    double lwe_std, glwe_std, pfks_std;
+    uint64_t max_noise_sq;
+
+    int K() const { return k * N; }                    // big LWE dimension
+    int M() const { return N / 2; }                    // Fourier coefficients per polynomial
+    size_t big_len() const { return (size_t)K() + 1; }  // big LWE size
+    size_t small_len() const { return (size_t)n + 1; }
+    size_t glwe_len() const { return (size_t)(k + 1) * N; }
+    size_t ksk_len() const { return (size_t)K() * ks_l * small_len(); }
+    size_t bsk_len() const { return (size_t)n * pbs_l * (k + 1) * glwe_len(); }
+    size_t bsk_fourier_len() const { return (size_t)n * pbs_l * (k + 1) * (k + 1) * M(); }
+    size_t pfpksk_len() const { return (size_t)(k + 1) * big_len() * pfks_l * glwe_len(); }
+    size_t cbs_ggsw_len() const { return (size_t)cbs_l * (k + 1) * glwe_len(); }
+    size_t cbs_ggsw_fourier_len() const { return (size_t)cbs_l * (k + 1) * (k + 1) * M(); }
+};
+
+enum ParamSet { SQRD_LVL_1 = 0, SQRD_LVL_4 = 1, SQRD_LVL_64 = 2, SQRD_LVL_256 = 3 };
+
+inline bool get_params(int id, Params &p) {
+    switch (id) {
+    case SQRD_LVL_1:  // parameters.rs:29-61
+        p = {id, 671, 2, 1024, 2, 15, 4, 3, 1, 10, 1, 24,
+             4.7280002450549286e-05, 3.162026630747649e-16, 3.162026630747649e-16, 1};
+        return true;
+    case SQRD_LVL_4:  // parameters.rs:77-109
+        p = {id, 679, 2, 1024, 2, 15, 4, 3, 1, 11, 2, 16,
+             4.7280002450549286e-05, 3.162026630747649e-16, 3.162026630747649e-16, 4};
+        return true;
+    case SQRD_LVL_64:  // parameters.rs:125-157
+        p = {id, 677, 4, 512, 3, 12, 4, 3, 1, 13, 2, 16,
+             4.7280002450549286e-05, 0.00000000000000022148688116005568,
+             0.00000000000000022148688116005568, 64};
+        return true;
+    case SQRD_LVL_256:  // parameters.rs:173-205
+        p = {id, 665, 2, 1024, 4, 9, 6, 2, 1, 14, 3, 12,
+             4.7280002450549286e-05, 3.162026630747649e-16, 3.162026630747649e-16, 256};
+        return true;
+    default:
+        return false;
+    }
+}
+
+}  // namespace tae

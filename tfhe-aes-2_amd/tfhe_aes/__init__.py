@@ -1,0 +1,17 @@
+"""tfhe_aes -- MI355X-native homomorphic AES-128 (1-bit WoP-PBS), host mirror of the reference crate.
+
+The crate name follows the reference (`tfhe_aes`, src/lib.rs); the compute path is the in-tree
+HIP library libtfhe_aes_amd.so (no CPU fallback).
+"""
+from ._native import (PARAMS_SQRD_LVL_1, PARAMS_SQRD_LVL_4, PARAMS_SQRD_LVL_64, PARAMS_SQRD_LVL_256, NoDevice,
+                      NoiseNotIndependent, NoiseTooBig, TaeError, device_count, get_params, lib)
+from .tfhe import (BitCt, ClientKey, Cleartext, FheContext, WopbsLUT, context_from_raw, decode_bit, encode_bit,
+                   generate_keys, generate_keys_raw)
+from . import aes_128
+
+__all__ = [
+    "PARAMS_SQRD_LVL_1", "PARAMS_SQRD_LVL_4", "PARAMS_SQRD_LVL_64", "PARAMS_SQRD_LVL_256", "NoDevice",
+    "NoiseNotIndependent", "NoiseTooBig", "TaeError", "device_count", "get_params", "lib", "BitCt", "ClientKey",
+    "Cleartext", "FheContext", "WopbsLUT", "context_from_raw", "decode_bit", "encode_bit", "generate_keys",
+    "generate_keys_raw", "aes_128",
+]

@@ -1,0 +1,208 @@
+"""AES-128 over the 1-bit WoP-PBS model -- Python mirror of the reference's `aes_128` module.
+
+Reference:
+  src/aes_128.rs                       Block/Key, SBOX, RC, ROUNDS, gf_256_mul (with its quirk)
+  src/aes_128/plain.rs                 plain AES with a `rounds` parameter (test oracle)
+  src/aes_128/fhe.rs:16-38             trait Aes128Encrypt {encrypt_block, encrypt_block_for_rounds, key_schedule}
+  src/aes_128/fhe/fhe_encryption.rs    client-side bytes <-> Byte<Bit>
+  src/aes_128/fhe/fhe_impls/shortint_woppbs_1bit.rs:131-151  ShortintWoppbs1BitSboxGalMulPbsAesEncrypt
+  src/util.rs:33-42                    MSB-first bit order
+The FHE round function runs on the GPU through the C-ABI (tae_aes_*).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Sequence
+
+import numpy as np
+
+from . import _native as N
+from ._native import check, lib
+from .tfhe import BitCt, ClientKey, Cleartext, FheContext, _handles
+
+ROUNDS = 10
+
+SBOX = [
+    0x63, 0x7c, 0x77, 0x7b, 0xf2, 0x6b, 0x6f, 0xc5, 0x30, 0x01, 0x67, 0x2b, 0xfe, 0xd7, 0xab, 0x76,
+    0xca, 0x82, 0xc9, 0x7d, 0xfa, 0x59, 0x47, 0xf0, 0xad, 0xd4, 0xa2, 0xaf, 0x9c, 0xa4, 0x72, 0xc0,
+    0xb7, 0xfd, 0x93, 0x26, 0x36, 0x3f, 0xf7, 0xcc, 0x34, 0xa5, 0xe5, 0xf1, 0x71, 0xd8, 0x31, 0x15,
+    0x04, 0xc7, 0x23, 0xc3, 0x18, 0x96, 0x05, 0x9a, 0x07, 0x12, 0x80, 0xe2, 0xeb, 0x27, 0xb2, 0x75,
+    0x09, 0x83, 0x2c, 0x1a, 0x1b, 0x6e, 0x5a, 0xa0, 0x52, 0x3b, 0xd6, 0xb3, 0x29, 0xe3, 0x2f, 0x84,
+    0x53, 0xd1, 0x00, 0xed, 0x20, 0xfc, 0xb1, 0x5b, 0x6a, 0xcb, 0xbe, 0x39, 0x4a, 0x4c, 0x58, 0xcf,
+    0xd0, 0xef, 0xaa, 0xfb, 0x43, 0x4d, 0x33, 0x85, 0x45, 0xf9, 0x02, 0x7f, 0x50, 0x3c, 0x9f, 0xa8,
+    0x51, 0xa3, 0x40, 0x8f, 0x92, 0x9d, 0x38, 0xf5, 0xbc, 0xb6, 0xda, 0x21, 0x10, 0xff, 0xf3, 0xd2,
+    0xcd, 0x0c, 0x13, 0xec, 0x5f, 0x97, 0x44, 0x17, 0xc4, 0xa7, 0x7e, 0x3d, 0x64, 0x5d, 0x19, 0x73,
+    0x60, 0x81, 0x4f, 0xdc, 0x22, 0x2a, 0x90, 0x88, 0x46, 0xee, 0xb8, 0x14, 0xde, 0x5e, 0x0b, 0xdb,
+    0xe0, 0x32, 0x3a, 0x0a, 0x49, 0x06, 0x24, 0x5c, 0xc2, 0xd3, 0xac, 0x62, 0x91, 0x95, 0xe4, 0x79,
+    0xe7, 0xc8, 0x37, 0x6d, 0x8d, 0xd5, 0x4e, 0xa9, 0x6c, 0x56, 0xf4, 0xea, 0x65, 0x7a, 0xae, 0x08,
+    0xba, 0x78, 0x25, 0x2e, 0x1c, 0xa6, 0xb4, 0xc6, 0xe8, 0xdd, 0x74, 0x1f, 0x4b, 0xbd, 0x8b, 0x8a,
+    0x70, 0x3e, 0xb5, 0x66, 0x48, 0x03, 0xf6, 0x0e, 0x61, 0x35, 0x57, 0xb9, 0x86, 0xc1, 0x1d, 0x9e,
+    0xe1, 0xf8, 0x98, 0x11, 0x69, 0xd9, 0x8e, 0x94, 0x9b, 0x1e, 0x87, 0xe9, 0xce, 0x55, 0x28, 0xdf,
+    0x8c, 0xa1, 0x89, 0x0d, 0xbf, 0xe6, 0x42, 0x68, 0x41, 0x99, 0x2d, 0x0f, 0xb0, 0x54, 0xbb, 0x16,
+]
+RC = [0x00, 0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80, 0x1B, 0x36]
+
+
+def gf_256_mul(a: int, b: int) -> int:
+    """aes_128.rs:42-56, including `if high_bit != 0x80 { a ^= 0x1b }`."""
+    res = 0
+    for _ in range(8):
+        if b & 1:
+            res ^= a
+        high = a & 0x80
+        a = (a << 1) & 0xFF
+        if high != 0x80:
+            a ^= 0x1B
+        b >>= 1
+    return res
+
+
+# ---------------------------------------------------------------- util.rs:33-42 ----
+def u8_to_bits(byte: int) -> List[int]:
+    return [1 if byte & (0x80 >> i) else 0 for i in range(8)]
+
+
+def bits_to_u8(bits: Sequence[int]) -> int:
+    return sum((int(b) & 1) << (7 - i) for i, b in enumerate(bits))
+
+
+# ---------------------------------------------------------------- plain.rs ----
+def key_schedule_plain(key: bytes) -> List[bytes]:
+    """plain::key_schedule (plain.rs:106-132): 44 words of 4 bytes."""
+    w = [bytes(key[4 * i:4 * i + 4]) for i in range(4)]
+    for i in range(4, 44):
+        t = list(w[i - 1])
+        if i % 4 == 0:
+            t = [SBOX[t[1]] ^ RC[i // 4], SBOX[t[2]], SBOX[t[3]], SBOX[t[0]]]
+        w.append(bytes(a ^ b for a, b in zip(w[i - 4], t)))
+    return w
+
+
+def encrypt_block_plain(expanded_key: Sequence[bytes], block: bytes, rounds: int = ROUNDS) -> bytes:
+    """plain::encrypt_block (plain.rs:75-103); the last round always uses words 40..44."""
+    rk = b"".join(expanded_key)
+    s = [block[i] ^ rk[i] for i in range(16)]
+    for r in range(1, rounds + 1):
+        last = r == rounds
+        s = [SBOX[x] for x in s]
+        t = [s[4 * ((c + row) % 4) + row] for c in range(4) for row in range(4)]
+        if not last:
+            m = []
+            for c in range(4):
+                col = t[4 * c:4 * c + 4]
+                m += [gf_256_mul(col[i], 2) ^ col[(i + 3) % 4] ^ col[(i + 2) % 4] ^ gf_256_mul(col[(i + 1) % 4], 3)
+                      for i in range(4)]
+            t = m
+        k = rk[160:176] if last else rk[16 * r:16 * r + 16]
+        s = [t[i] ^ k[i] for i in range(16)]
+    return bytes(s)
+
+
+def expand_key_and_encrypt_blocks(key: bytes, blocks: Sequence[bytes], rounds: int) -> List[bytes]:
+    ek = key_schedule_plain(key)
+    return [encrypt_block_plain(ek, b, rounds) for b in blocks]
+
+
+# ---------------------------------------------------------------- fhe_encryption.rs ----
+def encrypt_byte(client_key: ClientKey, byte: int) -> List[BitCt]:
+    return [client_key.encrypt(Cleartext(b)) for b in u8_to_bits(byte)]
+
+
+def encrypt_byte_array(client_key: ClientKey, array: bytes) -> List[List[BitCt]]:
+    return [encrypt_byte(client_key, b) for b in array]
+
+
+def encrypt_word_array(client_key: ClientKey, words: Sequence[bytes]) -> List[List[List[BitCt]]]:
+    return [encrypt_byte_array(client_key, w) for w in words]
+
+
+def decrypt_byte(client_key: ClientKey, byte: Sequence[BitCt]) -> int:
+    return bits_to_u8([client_key.decrypt(b).value for b in byte])
+
+
+def decrypt_byte_array(client_key: ClientKey, array) -> bytes:
+    return bytes(decrypt_byte(client_key, b) for b in array)
+
+
+def _flat_bits(x) -> List[BitCt]:
+    out = []
+
+    def rec(v):
+        if isinstance(v, BitCt):
+            out.append(v)
+        else:
+            for e in v:
+                rec(e)
+
+    rec(x)
+    return out
+
+
+# ---------------------------------------------------------------- Aes128Encrypt ----
+class ShortintWoppbs1BitSboxGalMulPbsAesEncrypt:
+    """fhe_impls/shortint_woppbs_1bit.rs:131-151 -- SBOX + GF x{1,2,3} by one 8->24 WoP-PBS."""
+
+    @staticmethod
+    def encrypt_block(ctx: FheContext, expanded_key, block):
+        return ShortintWoppbs1BitSboxGalMulPbsAesEncrypt.encrypt_block_for_rounds(ctx, expanded_key, block, ROUNDS)
+
+    @staticmethod
+    def encrypt_block_for_rounds(ctx: FheContext, expanded_key, block, rounds: int):
+        """expanded_key: [44][4][8] BitCt (nested or flat); block: [16][8] BitCt -> [16][8]."""
+        ek = _flat_bits(expanded_key)
+        blk = _flat_bits(block)
+        outs = (C.c_void_p * 128)()
+        check(lib().tae_aes_encrypt_block_for_rounds(ctx._h, _handles(ek), _handles(blk), rounds, outs))
+        bits = [BitCt(h, ctx) for h in outs]
+        return [bits[8 * i:8 * i + 8] for i in range(16)]
+
+    @staticmethod
+    def encrypt_blocks(ctx: FheContext, expanded_key, blocks, rounds: int = ROUNDS):
+        """Batched extension: all blocks' SBOXes of a round go to the GPU as one batch."""
+        ek = _flat_bits(expanded_key)
+        flat = _flat_bits(blocks)
+        nb = len(flat) // 128
+        outs = (C.c_void_p * (128 * nb))()
+        check(lib().tae_aes_encrypt_blocks(ctx._h, _handles(ek), _handles(flat), nb, rounds, outs))
+        bits = [BitCt(h, ctx) for h in outs]
+        return [[bits[b * 128 + 8 * i:b * 128 + 8 * i + 8] for i in range(16)] for b in range(nb)]
+
+    @staticmethod
+    def key_schedule(ctx: FheContext, key):
+        """fhe_sbox_gal_mul_pbs::key_schedule (:134-164): [16][8] BitCt -> [44][4][8]."""
+        kb = _flat_bits(key)
+        outs = (C.c_void_p * (44 * 32))()
+        check(lib().tae_aes_key_schedule(ctx._h, _handles(kb), outs))
+        bits = [BitCt(h, ctx) for h in outs]
+        return [[bits[w * 32 + 8 * b:w * 32 + 8 * b + 8] for b in range(4)] for w in range(44)]
+
+    @staticmethod
+    def encrypt_blocks_raw(ctx: FheContext, rk: np.ndarray, blocks: np.ndarray, rounds: int = ROUNDS) -> np.ndarray:
+        """Host arrays: rk [1408][K+1], blocks [n][128][K+1] -> [n][128][K+1]."""
+        rk = np.ascontiguousarray(rk, dtype=np.uint64)
+        blocks = np.ascontiguousarray(blocks, dtype=np.uint64)
+        nb = blocks.shape[0]
+        out = np.zeros_like(blocks)
+        check(lib().tae_aes_encrypt_blocks_raw(ctx._h, rk.ctypes.data_as(C.c_void_p), blocks.ctypes.data_as(C.c_void_p),
+                                               nb, rounds, out.ctypes.data_as(C.c_void_p), N.TAE_MEM_HOST))
+        return out
+
+    @staticmethod
+    def encrypt_blocks_device(ctx: FheContext, d_rk: int, d_blocks: int, nb: int, rounds: int, d_out: int):
+        """Device pointers (ints), inputs resident in HBM."""
+        check(lib().tae_aes_encrypt_blocks_raw(ctx._h, C.c_void_p(d_rk), C.c_void_p(d_blocks), nb, rounds,
+                                               C.c_void_p(d_out), N.TAE_MEM_DEVICE))
+
+
+def counter_blocks(iv: bytes, count: int) -> List[bytes]:
+    """main.rs:108-115: block = iv (8 bytes) || ctr as u64 big-endian, ctr = 1..=count."""
+    return [bytes(iv) + c.to_bytes(8, "big") for c in range(1, count + 1)]
+
+
+def blocks_to_bits(blocks: Sequence[bytes]) -> np.ndarray:
+    return np.array([[b for byte in blk for b in u8_to_bits(byte)] for blk in blocks], dtype=np.uint8)
+
+
+def bits_to_blocks(bits: np.ndarray) -> List[bytes]:
+    bits = np.asarray(bits).reshape(-1, 16, 8)
+    return [bytes(bits_to_u8(byte) for byte in blk) for blk in bits]

@@ -1,0 +1,267 @@
+"""Python mirror of the reference's `tfhe_aes::tfhe` model API over the C-ABI.
+
+Reference: src/tfhe.rs:11-24 (ClientKeyT / ContextT) and src/tfhe/shortint_woppbs_1bit.rs
+(BitCt :26-151, FheContext :165-336, ClientKey :189-226, encode/decode :125-132).  Names follow the
+reference so tests read like its own (`client_key.encrypt(Cleartext(1))`, `context.circuit_bootstrap`).
+All ciphertext arithmetic happens in libtfhe_aes_amd.so on the GPU; this module only marshals.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from typing import Callable, Sequence
+
+import numpy as np
+
+from . import _native as N
+from ._native import check, lib
+
+__all__ = ["Cleartext", "BitCt", "FheContext", "ClientKey", "WopbsLUT", "encode_bit", "decode_bit",
+           "generate_keys", "generate_keys_raw"]
+
+
+@dataclass(frozen=True)
+class Cleartext:
+    value: int
+
+    def __getitem__(self, i):  # Cleartext(..).0 in Rust
+        assert i == 0
+        return self.value
+
+
+def encode_bit(bit: Cleartext) -> int:
+    """shortint_woppbs_1bit.rs:125-128"""
+    assert bit.value < 2, f"cleartext out of bounds: {bit.value}"
+    return (bit.value << 63) & 0xFFFFFFFFFFFFFFFF
+
+
+def decode_bit(encoding: int) -> Cleartext:
+    """shortint_woppbs_1bit.rs:130-132"""
+    return Cleartext((((encoding + (1 << 62)) & 0xFFFFFFFFFFFFFFFF) & (1 << 63)) >> 63)
+
+
+class BitCt:
+    """Handle to a shortint_woppbs_1bit::BitCt (LWE under the big key + noise bookkeeping)."""
+
+    __slots__ = ("_h", "context")
+
+    def __init__(self, handle, context: "FheContext | None"):
+        self._h = C.c_void_p(handle)
+        self.context = context
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().tae_bit_free(self._h)
+                self._h = C.c_void_p(None)
+        except Exception:
+            pass
+
+    def clone(self) -> "BitCt":
+        out = C.c_void_p()
+        check(lib().tae_bit_clone(self._h, C.byref(out)))
+        return BitCt(out.value, self.context)
+
+    def __ixor__(self, rhs: "BitCt") -> "BitCt":  # BitXorAssign (:134-142)
+        check(lib().tae_bit_xor_assign(self._h, rhs._h))
+        return self
+
+    def __xor__(self, rhs: "BitCt") -> "BitCt":  # BitXor (:144-151): consumes self in Rust
+        out = self.clone()
+        out ^= rhs
+        return out
+
+    @property
+    def noise_level_squared(self) -> int:
+        v = C.c_uint64()
+        check(lib().tae_bit_noise_level(self._h, C.byref(v)))
+        return v.value
+
+    def data(self, lwe_size: int) -> np.ndarray:
+        arr = np.zeros(lwe_size, dtype=np.uint64)
+        check(lib().tae_bit_data(self._h, arr.ctypes.data_as(C.c_void_p), lwe_size))
+        return arr
+
+
+def _handles(bits: Sequence[BitCt]):
+    arr = (C.c_void_p * len(bits))()
+    for i, b in enumerate(bits):
+        arr[i] = b._h.value
+    return arr
+
+
+class WopbsLUT:
+    """tfhe::shortint::wopbs::WopbsLUTBase produced by FheContext::generate_lookup_table."""
+
+    def __init__(self, handle, input_bits: int, output_bits: int):
+        self._h = C.c_void_p(handle)
+        self.input_bits = input_bits
+        self.output_bits = output_bits
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().tae_lut_free(self._h)
+        except Exception:
+            pass
+
+    def as_array(self) -> np.ndarray:
+        n = C.c_size_t()
+        check(lib().tae_lut_data(self._h, None, 0, C.byref(n)))
+        arr = np.zeros(n.value, dtype=np.uint64)
+        check(lib().tae_lut_data(self._h, arr.ctypes.data_as(C.c_void_p), n.value, None))
+        return arr
+
+    def get_small_lut(self, j: int) -> np.ndarray:
+        a = self.as_array()
+        small = a.size // self.output_bits
+        return a[j * small:(j + 1) * small]
+
+
+class FheContext:
+    """shortint_woppbs_1bit::FheContext -- server side, bound to one GPU."""
+
+    def __init__(self, handle, param_set: int):
+        self._h = C.c_void_p(handle)
+        self.param_set = param_set
+        p = N.TaeParams()
+        check(lib().tae_context_params(self._h, C.byref(p)))
+        self.params = p.as_dict()
+        self.lwe_size = self.params["k"] * self.params["N"] + 1
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().tae_context_free(self._h)
+        except Exception:
+            pass
+
+    # ContextT::trivial (src/tfhe.rs:20-24)
+    def trivial(self, bit: Cleartext) -> BitCt:
+        out = C.c_void_p()
+        check(lib().tae_trivial(self._h, bit.value, C.byref(out)))
+        return BitCt(out.value, self)
+
+    def bit_from_data(self, data: np.ndarray, noise_level_squared: int = 1) -> BitCt:
+        data = np.ascontiguousarray(data, dtype=np.uint64)
+        out = C.c_void_p()
+        check(lib().tae_bit_from_data(self._h, data.ctypes.data_as(C.c_void_p), data.size,
+                                      noise_level_squared, C.byref(out)))
+        return BitCt(out.value, self)
+
+    # generate_lookup_table (:274-289)
+    def generate_lookup_table(self, input_bits: int, output_bits: int, f: Callable[[int], int]) -> WopbsLUT:
+        tab = np.array([f(v) & 0xFFFFFFFFFFFFFFFF for v in range(1 << input_bits)], dtype=np.uint64)
+        out = C.c_void_p()
+        check(lib().tae_generate_lookup_table(self._h, input_bits, output_bits, tab.ctypes.data_as(C.c_void_p),
+                                              C.byref(out)))
+        return WopbsLUT(out.value, input_bits, output_bits)
+
+    # circuit_bootstrap (:292-336)
+    def circuit_bootstrap(self, bits: Sequence[BitCt], lut: WopbsLUT) -> list:
+        outs = (C.c_void_p * lut.output_bits)()
+        check(lib().tae_circuit_bootstrap(self._h, _handles(bits), len(bits), lut._h, outs))
+        return [BitCt(h, self) for h in outs]
+
+    def circuit_bootstrap_raw(self, bits: np.ndarray, lut: WopbsLUT) -> np.ndarray:
+        """Batched: bits [groups][n_in][K+1] -> [groups][n_out][K+1] (host arrays)."""
+        bits = np.ascontiguousarray(bits, dtype=np.uint64)
+        groups, n_in = bits.shape[0], bits.shape[1]
+        out = np.zeros((groups, lut.output_bits, self.lwe_size), dtype=np.uint64)
+        check(lib().tae_circuit_bootstrap_raw(self._h, bits.ctypes.data_as(C.c_void_p), groups, n_in, lut._h,
+                                              out.ctypes.data_as(C.c_void_p), N.TAE_MEM_HOST))
+        return out
+
+    def synchronize(self):
+        check(lib().tae_synchronize(self._h))
+
+    def set_timing(self, on: bool):
+        check(lib().tae_set_timing(self._h, 1 if on else 0))
+
+    def last_stage_times(self) -> dict:
+        arr = (C.c_float * 5)()
+        check(lib().tae_last_stage_times(self._h, arr))
+        return dict(zip(("keyswitch", "pbs", "pfks", "ggsw_fft", "vertical_packing"), list(arr)))
+
+
+class ClientKey:
+    """shortint_woppbs_1bit::ClientKey (ClientKeyT, src/tfhe.rs:11-18)."""
+
+    def __init__(self, handle, param_set: int, context: FheContext | None = None):
+        self._h = C.c_void_p(handle)
+        self.param_set = param_set
+        self.context = context
+        self.params = N.get_params(param_set)
+        self.lwe_size = self.params["k"] * self.params["N"] + 1
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().tae_client_key_free(self._h)
+        except Exception:
+            pass
+
+    def encrypt(self, bit: Cleartext) -> BitCt:
+        out = C.c_void_p()
+        check(lib().tae_encrypt(self._h, bit.value, C.byref(out)))
+        return BitCt(out.value, self.context)
+
+    def decrypt(self, bit: BitCt) -> Cleartext:
+        v = C.c_uint64()
+        check(lib().tae_decrypt(self._h, bit._h, C.byref(v)))
+        return Cleartext(v.value)
+
+    def encrypt_bits_raw(self, bits, start_index: int) -> np.ndarray:
+        bits = np.ascontiguousarray(np.asarray(bits, dtype=np.uint8).ravel())
+        out = np.zeros((bits.size, self.lwe_size), dtype=np.uint64)
+        check(lib().tae_encrypt_bits_raw(self._h, bits.ctypes.data_as(C.c_void_p), bits.size, start_index,
+                                         out.ctypes.data_as(C.c_void_p)))
+        return out
+
+    def decrypt_bits_raw(self, cts: np.ndarray) -> np.ndarray:
+        cts = np.ascontiguousarray(cts, dtype=np.uint64).reshape(-1, self.lwe_size)
+        out = np.zeros(cts.shape[0], dtype=np.uint8)
+        check(lib().tae_decrypt_bits_raw(self._h, cts.ctypes.data_as(C.c_void_p), cts.shape[0],
+                                         out.ctypes.data_as(C.c_void_p)))
+        return out
+
+    def secrets(self):
+        p = self.params
+        lwe = np.zeros(p["n"], dtype=np.uint64)
+        glwe = np.zeros(p["k"] * p["N"], dtype=np.uint64)
+        check(lib().tae_client_key_secrets(self._h, lwe.ctypes.data_as(C.c_void_p), glwe.ctypes.data_as(C.c_void_p)))
+        return lwe, glwe
+
+
+def generate_keys(param_set: int = N.PARAMS_SQRD_LVL_64, seed: bytes | None = None, device: int = 0,
+                  threads: int | None = None):
+    """FheContext::generate_keys_with_params (shortint_woppbs_1bit.rs:245-268) -> (ClientKey, FheContext)."""
+    seed = os.urandom(32) if seed is None else bytes(seed)
+    assert len(seed) == 32
+    threads = threads or min(16, os.cpu_count() or 1)
+    ck, ctx = C.c_void_p(), C.c_void_p()
+    check(lib().tae_generate_keys(param_set, seed, device, threads, C.byref(ck), C.byref(ctx)))
+    context = FheContext(ctx.value, param_set)
+    return ClientKey(ck.value, param_set, context), context
+
+
+def generate_keys_raw(param_set: int = N.PARAMS_SQRD_LVL_64, seed: bytes | None = None, threads: int | None = None):
+    """Client key + standard-domain server key arrays (ksk, bsk, pfpksk) on the host."""
+    seed = os.urandom(32) if seed is None else bytes(seed)
+    threads = threads or min(16, os.cpu_count() or 1)
+    sizes = [C.c_size_t() for _ in range(3)]
+    check(lib().tae_server_key_sizes(param_set, *[C.byref(s) for s in sizes]))
+    ksk, bsk, pfpksk = (np.zeros(s.value, dtype=np.uint64) for s in sizes)
+    ck = C.c_void_p()
+    check(lib().tae_generate_keys_raw(param_set, seed, threads, C.byref(ck), ksk.ctypes.data_as(C.c_void_p),
+                                      bsk.ctypes.data_as(C.c_void_p), pfpksk.ctypes.data_as(C.c_void_p)))
+    return ClientKey(ck.value, param_set), (ksk, bsk, pfpksk)
+
+
+def context_from_raw(param_set: int, keys, device: int = 0, mem: int = N.TAE_MEM_HOST) -> FheContext:
+    """Server context from raw keys: numpy arrays (mem=HOST) or device pointers as ints (mem=DEVICE)."""
+    ptrs = [k.ctypes.data_as(C.c_void_p) if isinstance(k, np.ndarray) else C.c_void_p(int(k)) for k in keys]
+    ctx = C.c_void_p()
+    check(lib().tae_context_create_raw(param_set, device, ptrs[0], ptrs[1], ptrs[2], mem, C.byref(ctx)))
+    return FheContext(ctx.value, param_set)
