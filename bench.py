@@ -1,0 +1,246 @@
+#!/usr/bin/env python3
+"""FHE AES-128 counter-mode throughput on MI355X (BASELINE.json metric: FHE AES-128 blocks/sec).
+
+One step = one full 10-round homomorphic AES-128 (fhe_sbox_gal_mul_pbs::encrypt_block_for_rounds,
+ShortintWoppbs1BitSboxGalMulPbsAesEncrypt, params_sqrd_lvl_64) of this rank's batch of counter blocks
+(default 128 per GPU = BASELINE configs[2]; at 8 GPUs 1024 blocks = configs[3]).  Inputs (encrypted
+blocks + FHE-expanded round key) are resident in HBM before the timed region; outputs are decrypted
+and checked against plain AES after it.  The FHE key schedule (main.rs:130-139) runs once and is
+reported separately (key_expansion_s), as in the reference.
+
+Multi-GPU: `python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`: blocks shard across
+ranks (weak scaling); the server keys (KSK, BSK, PFPKSK: 672 MB) and the expanded round key are
+broadcast once from rank 0 over RCCL (torch.distributed "nccl") before timing; no collective on the
+data path.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "tfhe-aes-2_amd"))
+sys.path.insert(0, ROOT)
+
+SEED = bytes(range(32))
+README_KEY = bytes.fromhex("76b8e0ada0f13d90405d6ae55386bd28")  # README / main.rs scenario
+README_IV = bytes.fromhex("bdd219b8a08ded1a")
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
+FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (= FP64 matrix) dense peak, spec
+
+
+def pbs_algorithmic(p, bits):
+    """Per-launch algorithmic figures of the PBS kernel: the Fourier BSK streamed once,
+    every small LWE read, every big LWE written; FP64 = 677 CMux x (20 FFT x (5 M log2 M + 6 M) +
+    75 x M x 8) per bootstrap."""
+    M = p["N"] // 2
+    logM = M.bit_length() - 1
+    rows = (p["k"] + 1) * p["pbs_l"]
+    bsk_bytes = p["n"] * rows * (p["k"] + 1) * M * 16
+    io_bytes = bits * ((p["n"] + 1) + (p["k"] * p["N"] + 1)) * 8
+    ffts = rows + (p["k"] + 1)
+    flop_cmux = ffts * (5 * M * logM + 6 * M) + rows * (p["k"] + 1) * M * 8
+    return bsk_bytes + io_bytes, p["n"] * flop_cmux * bits
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--blocks-per-gpu", type=int, default=128)
+    ap.add_argument("--rounds", type=int, default=10)
+    ap.add_argument("--key-schedule", choices=["fhe", "plain"], default="fhe")
+    ap.add_argument("--cpu-baseline", choices=["auto", "on", "off"], default="auto")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    import torch  # plumbing: device memory + torch.distributed (nccl == RCCL)
+    import tfhe_aes
+    from tfhe_aes import aes_128
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = local
+    torch.cuda.set_device(dev)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+    threads = min(16, os.cpu_count() or 1)
+    pid = tfhe_aes.PARAMS_SQRD_LVL_64
+    p = tfhe_aes.get_params(pid)
+    L = p["k"] * p["N"] + 1
+
+    # ---- keys: generated on rank 0 (client side), server keys broadcast once over RCCL ----
+    t = time.time()
+    sizes = None
+    if rank == 0:
+        ck0, raw = tfhe_aes.generate_keys_raw(pid, SEED, threads=threads)
+    keygen_s = time.time() - t
+    ck = tfhe_aes.client_key_from_seed(pid, SEED)
+    t = time.time()
+    if world == 1:
+        ctx = tfhe_aes.context_from_raw(pid, raw, device=dev)
+    else:
+        from tfhe_aes import _native as N
+        lens = [C.c_size_t() for _ in range(3)]
+        N.check(N.lib().tae_server_key_sizes(pid, *[C.byref(x) for x in lens]))
+        bufs = []
+        for i, n in enumerate(lens):
+            if rank == 0:
+                tt = torch.from_numpy(raw[i].view(np.int64)).to(f"cuda:{dev}")
+            else:
+                tt = torch.empty(n.value, dtype=torch.int64, device=f"cuda:{dev}")
+            dist.broadcast(tt, src=0)
+            bufs.append(tt)
+        torch.cuda.synchronize()
+        ctx = tfhe_aes.context_from_raw(pid, [b.data_ptr() for b in bufs], device=dev, mem=1)
+        ctx._keepalive = bufs
+    key_setup_s = time.time() - t
+
+    # ---- expanded key: FHE key schedule on rank 0 (timed separately), broadcast ----
+    t = time.time()
+    rk_np = None
+    if rank == 0:
+        if args.key_schedule == "fhe":
+            key_bits = aes_128.encrypt_byte_array(ck, README_KEY)
+            ek = aes_128.ShortintWoppbs1BitSboxGalMulPbsAesEncrypt.key_schedule(ctx, key_bits)
+            rk_np = np.stack([b.data(L) for w in ek for byte in w for b in byte])
+            assert b"".join(aes_128.decrypt_byte_array(ck, w) for w in ek) == b"".join(
+                aes_128.key_schedule_plain(README_KEY)), "FHE key schedule mismatch"
+        else:
+            ek = b"".join(aes_128.key_schedule_plain(README_KEY))
+            rk_np = ck.encrypt_bits_raw([b for byte in ek for b in aes_128.u8_to_bits(byte)], start_index=1 << 40)
+    key_expansion_s = time.time() - t
+    if rank == 0:
+        rk_dev = torch.from_numpy(rk_np.view(np.int64)).to(f"cuda:{dev}")
+    else:
+        rk_dev = torch.empty((44 * 32, L), dtype=torch.int64, device=f"cuda:{dev}")
+    if world > 1:
+        dist.broadcast(rk_dev, src=0)
+
+    # ---- this rank's counter blocks (main.rs:108-115), encrypted client side, resident in HBM ----
+    nb = args.blocks_per_gpu
+    ctrs = range(rank * nb + 1, (rank + 1) * nb + 1)
+    blocks = [README_IV + c.to_bytes(8, "big") for c in ctrs]
+    t = time.time()
+    bits = aes_128.blocks_to_bits(blocks)
+    cts = ck.encrypt_bits_raw(bits, start_index=(1 << 32) + rank * nb * 128)
+    encrypt_s = time.time() - t
+    blk_dev = torch.from_numpy(cts.view(np.int64)).to(f"cuda:{dev}")
+    out_dev = torch.empty_like(blk_dev)
+    torch.cuda.synchronize()
+    E = aes_128.ShortintWoppbs1BitSboxGalMulPbsAesEncrypt
+
+    def step():
+        E.encrypt_blocks_device(ctx, rk_dev.data_ptr(), blk_dev.data_ptr(), nb, args.rounds, out_dev.data_ptr())
+
+    for _ in range(args.warmup):
+        step()
+    ctx.set_timing(True)
+    stage_ms = {}
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ctx.synchronize()
+    t0 = time.time()
+    for _ in range(args.steps):
+        step()
+        for kk, v in ctx.last_stage_times().items():
+            stage_ms[kk] = stage_ms.get(kk, 0.0) + v
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.time() - t0
+    ctx.set_timing(False)
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    # ---- correctness gate: decrypt and compare with plain AES (outside the timed region) ----
+    out = out_dev.cpu().numpy().view(np.uint64)
+    got = aes_128.bits_to_blocks(ck.decrypt_bits_raw(out))
+    ek_plain = aes_128.key_schedule_plain(README_KEY)
+    ok = int(all(g == aes_128.encrypt_block_plain(ek_plain, b, args.rounds) for g, b in zip(got, blocks)))
+    if dist:
+        tt = torch.tensor([ok], dtype=torch.int32, device=f"cuda:{dev}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MIN)
+        ok = int(tt.item())
+    if not ok:
+        raise SystemExit(f"rank {rank}: decrypted AES output differs from plain AES")
+
+    total_blocks = nb * world * args.steps
+    value = total_blocks / elapsed
+    ms_per_step = elapsed * 1000.0 / args.steps
+
+    # ---- roofline of the dominant kernel (PBS = homomorphic_shift_boolean blind rotation) ----
+    launches = args.steps * args.rounds * p["cbs_l"]
+    pbs_ms = stage_ms.get("pbs", 0.0) / max(launches, 1)
+    bytes_launch, flop_launch = pbs_algorithmic(p, nb * 16 * 8)
+    gbs = bytes_launch / (pbs_ms * 1e-3) / 1e9 if pbs_ms > 0 else None
+    tflops = flop_launch / (pbs_ms * 1e-3) / 1e12 if pbs_ms > 0 else None
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_pbs_latest.json")
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as fh:
+            pm = json.load(fh)
+        if pm.get("bits_per_launch") == nb * 16 * 8:
+            traffic = pm.get("hbm_bytes_per_launch")
+    roofline = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": (gbs / HBM_PEAK_GBS) if gbs else None, "traffic": traffic,
+                "kernel": "pbs_kernel<512> (homomorphic_shift_boolean)", "avg_launch_ms": pbs_ms,
+                "algorithmic_bytes_per_launch": bytes_launch,
+                "fp64": {"achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": (tflops / FP64_PEAK_TFLOPS) if tflops else None,
+                         "algorithmic_flop_per_launch": flop_launch}}
+    stage_share = {k: v / args.steps for k, v in stage_ms.items()}
+
+    cpu = None
+    want_cpu = args.cpu_baseline == "on" or (args.cpu_baseline == "auto" and world == 1)
+    if want_cpu and rank == 0:
+        cpu = cpu_baseline(raw, ck, min(args.cpu_threads, os.cpu_count() or 1))
+
+    if rank == 0:
+        rec = {"metric": "FHE AES-128 blocks/sec", "value": value, "unit": "blocks/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "u64 torus / f64 FFT", "data": "synthetic",
+               "config": {"workload": f"{nb} counter-mode blocks per GPU, 10-round FHE AES-128 "
+                                      "(ShortintWoppbs1BitSboxGalMulPbsAesEncrypt, params_sqrd_lvl_64)",
+                          "blocks_per_gpu": nb, "global_blocks": nb * world, "rounds": args.rounds,
+                          "parallelism": f"blocks sharded over {world} GPU(s), keys broadcast once"},
+               "roofline": roofline, "cpu_baseline": cpu,
+               "stage_ms_per_step": stage_share, "per_sbox_ms": ms_per_step / (nb * 16 * args.rounds),
+               "keygen_s": keygen_s, "key_setup_s": key_setup_s, "key_expansion_s": key_expansion_s,
+               "encrypt_s": encrypt_s, "correct": bool(ok)}
+        print(json.dumps(rec), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(raw, ck, threads):
+    """CPU oracle (restatement, kind "port") on a bounded sample of the same workload: the 16 SBOX
+    circuit bootstraps of one AES round of one block, threads over bytes as the reference's rayon
+    (fhe_sbox_gal_mul_pbs.rs:33-41); blocks/s = 1 / (10 x round time)."""
+    from oracle import oracle
+    from tfhe_aes import aes_128
+    ok = oracle.Keys(oracle.PARAMS_SQRD_LVL_64, None, raw=raw)
+    blk = README_IV + (1).to_bytes(8, "big")
+    cts = ck.encrypt_bits_raw(aes_128.blocks_to_bits([blk]), start_index=7 << 40)
+    t = time.time()
+    ok.sub_bytes_gal_mul(cts, threads)
+    dt = time.time() - t
+    return {"value": 1.0 / (10 * dt), "unit": "blocks/s", "cores": threads, "kind": "port",
+            "sample": f"16 SBOX 8->24 circuit bootstraps (one AES round of one block) on {threads} threads "
+                      f"in {dt:.2f} s, x10 rounds"}
+
+
+if __name__ == "__main__":
+    main()

@@ -72,6 +72,9 @@ int tae_server_key_sizes(int param_set, size_t *ksk_len, size_t *bsk_len, size_t
 int tae_generate_keys_raw(int param_set, const uint8_t seed[32], int threads,
                           tae_client_key **client_key, uint64_t *ksk, uint64_t *bsk,
                           uint64_t *pfpksk);
+/* Client key only (secret keys from the seed's LWE_SK / GLWE_SK streams; no server keys) -- every rank
+ * of a multi-GPU run derives the same client key this way while server keys are broadcast. */
+int tae_client_key_from_seed(int param_set, const uint8_t seed[32], tae_client_key **client_key);
 /* Server context from raw keys: mem = TAE_MEM_HOST (copied to the device) or TAE_MEM_DEVICE
  * (device pointers on `device`, e.g. after an RCCL broadcast; they must outlive the context). */
 int tae_context_create_raw(int param_set, int device, const uint64_t *ksk, const uint64_t *bsk,

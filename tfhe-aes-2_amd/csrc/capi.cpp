@@ -182,6 +182,15 @@ int tae_generate_keys(int param_set, const uint8_t seed[32], int device, int thr
     });
 }
 
+int tae_client_key_from_seed(int param_set, const uint8_t seed[32], tae_client_key **client_key) {
+    return guarded([&] {
+        require(seed && client_key, "null argument");
+        auto ck = std::make_unique<tae_client_key>();
+        tae::generate_client_key(params_of(param_set), seed, ck->ck);
+        *client_key = ck.release();
+    });
+}
+
 int tae_context_create_raw(int param_set, int device, const uint64_t *ksk, const uint64_t *bsk,
                            const uint64_t *pfpksk, int mem, tae_context **context) {
     return guarded([&] {

@@ -134,9 +134,8 @@ uint64_t ClientKey::phase(const uint64_t *ct) const {
     return ct[K] - s;
 }
 
-void generate_keys(const Params &p, const uint8_t seed[32], int threads, ClientKey &ck,
-                   ServerKeyRaw &sk) {
-    const int n = p.n, k = p.k, N = p.N, K = p.K();
+void generate_client_key(const Params &p, const uint8_t seed[32], ClientKey &ck) {
+    const int n = p.n, K = p.K();
     ck.p = p;
     std::memcpy(ck.seed.data(), seed, 32);
     ck.lwe_sk.assign(n, 0);
@@ -156,6 +155,12 @@ void generate_keys(const Params &p, const uint8_t seed[32], int threads, ClientK
         }
         for (int i = 0; i < K; i++) ck.glwe_sk[i] = bytes[i] & 1;
     }
+}
+
+void generate_keys(const Params &p, const uint8_t seed[32], int threads, ClientKey &ck,
+                   ServerKeyRaw &sk) {
+    const int n = p.n, k = p.k, N = p.N, K = p.K();
+    generate_client_key(p, seed, ck);
     sk.p = p;
     sk.ksk.assign(p.ksk_len(), 0);
     sk.bsk.assign(p.bsk_len(), 0);

@@ -66,6 +66,9 @@ struct ClientKey {
 void generate_keys(const Params &p, const uint8_t seed[32], int threads, ClientKey &ck,
                    ServerKeyRaw &sk);
 
+// secret keys only (same streams as generate_keys)
+void generate_client_key(const Params &p, const uint8_t seed[32], ClientKey &ck);
+
 // generate_multivariate_luts: out [output_bits][N << tree_bits]
 size_t lut_small_len(int N, int input_bits);
 void generate_lut(int N, int input_bits, int output_bits, const uint64_t *f_table, uint64_t *out);

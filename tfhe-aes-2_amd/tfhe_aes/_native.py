@@ -19,7 +19,7 @@ PARAMS_SQRD_LVL_1, PARAMS_SQRD_LVL_4, PARAMS_SQRD_LVL_64, PARAMS_SQRD_LVL_256 = 
 # Every symbol include/tfhe_aes_gpu.h declares (checked by tests/test_capi_symbols.py).
 EXPORTED = [
     "tae_last_error", "tae_version", "tae_device_count", "tae_get_params", "tae_generate_keys",
-    "tae_server_key_sizes", "tae_generate_keys_raw", "tae_context_create_raw", "tae_context_free",
+    "tae_server_key_sizes", "tae_generate_keys_raw", "tae_client_key_from_seed", "tae_context_create_raw", "tae_context_free",
     "tae_client_key_free", "tae_client_key_secrets", "tae_context_params", "tae_encrypt", "tae_decrypt",
     "tae_trivial", "tae_encrypt_bits_raw", "tae_decrypt_bits_raw", "tae_bit_clone", "tae_bit_free",
     "tae_bit_xor_assign", "tae_bit_noise_level", "tae_bit_data", "tae_bit_from_data",
@@ -81,6 +81,7 @@ def lib() -> C.CDLL:
         "tae_generate_keys": ([C.c_int, C.c_char_p, C.c_int, C.c_int, vpp, vpp], C.c_int),
         "tae_server_key_sizes": ([C.c_int, C.POINTER(sz), C.POINTER(sz), C.POINTER(sz)], C.c_int),
         "tae_generate_keys_raw": ([C.c_int, C.c_char_p, C.c_int, vpp, vp, vp, vp], C.c_int),
+        "tae_client_key_from_seed": ([C.c_int, C.c_char_p, vpp], C.c_int),
         "tae_context_create_raw": ([C.c_int, C.c_int, vp, vp, vp, C.c_int, vpp], C.c_int),
         "tae_context_free": ([vp], None), "tae_client_key_free": ([vp], None),
         "tae_client_key_secrets": ([vp, vp, vp], C.c_int),

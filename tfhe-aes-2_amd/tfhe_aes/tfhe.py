@@ -18,7 +18,7 @@ from . import _native as N
 from ._native import check, lib
 
 __all__ = ["Cleartext", "BitCt", "FheContext", "ClientKey", "WopbsLUT", "encode_bit", "decode_bit",
-           "generate_keys", "generate_keys_raw"]
+           "generate_keys", "generate_keys_raw", "client_key_from_seed", "context_from_raw"]
 
 
 @dataclass(frozen=True)
@@ -257,6 +257,13 @@ def generate_keys_raw(param_set: int = N.PARAMS_SQRD_LVL_64, seed: bytes | None 
     check(lib().tae_generate_keys_raw(param_set, seed, threads, C.byref(ck), ksk.ctypes.data_as(C.c_void_p),
                                       bsk.ctypes.data_as(C.c_void_p), pfpksk.ctypes.data_as(C.c_void_p)))
     return ClientKey(ck.value, param_set), (ksk, bsk, pfpksk)
+
+
+def client_key_from_seed(param_set: int, seed: bytes) -> ClientKey:
+    """Secret keys only, from the same seed streams as generate_keys_raw."""
+    ck = C.c_void_p()
+    check(lib().tae_client_key_from_seed(param_set, bytes(seed), C.byref(ck)))
+    return ClientKey(ck.value, param_set)
 
 
 def context_from_raw(param_set: int, keys, device: int = 0, mem: int = N.TAE_MEM_HOST) -> FheContext:
