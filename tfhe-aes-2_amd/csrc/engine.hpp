@@ -108,6 +108,8 @@ class Engine {
     cplx *d_ggsw_f_ = nullptr;
     size_t cap_small_ = 0, cap_big_ = 0, cap_ggsw_ = 0, cap_ggsw_f_ = 0, cap_state_ = 0, cap_muls_ = 0;
     hipEvent_t ev_[8];
+    double w16_[10] = {};     // W_16^{1,2,3,6,9} from the FFT table (batched N=512 kernels)
+    bool batched512_ = false; // N == 512, k == 4: multi-ciphertext blind-rotation kernels
     bool timing_ = false;
     StageTimes times_;
 };

@@ -17,6 +17,7 @@
 #include <stdexcept>
 
 #include "aes.hpp"
+#include "br512.hpp"
 #include "engine.hpp"
 #include "fft_device.hpp"
 
@@ -405,6 +406,18 @@ __global__ void lwe_add_kernel(uint64_t *__restrict__ a, const uint64_t *__restr
 
 unsigned grid_for(size_t total) { return (unsigned)std::min<size_t>((total + kThreads - 1) / kThreads, 65536); }
 
+constexpr int kBrC = 3;  // ciphertexts per workgroup in the batched N=512 blind rotation
+
+br512::W16 make_w16(const double *w) {
+    br512::W16 W;
+    W.w1 = {w[0], w[1]};
+    W.w2 = {w[2], w[3]};
+    W.w3 = {w[4], w[5]};
+    W.w6 = {w[6], w[7]};
+    W.w9 = {w[8], w[9]};
+    return W;
+}
+
 template <int N>
 size_t br_lds_bytes(int k, int levels) {
     return (size_t)(k + 1) * N * 8 + (size_t)(k + 1) * levels * (N / 2) * 16 + (size_t)(k + 1) * (N / 2) * 16;
@@ -467,6 +480,20 @@ void Engine::init_common() {
     d_lut8_ = static_cast<uint64_t *>(alloc(l8.size() * 8));
     HIPC(hipMemcpy(d_lut24_, l24.data(), l24.size() * 8, hipMemcpyHostToDevice));
     HIPC(hipMemcpy(d_lut8_, l8.data(), l8.size() * 8, hipMemcpyHostToDevice));
+    // batched N=512 blind rotation (br512.hpp); TAE_BR_V1=1 forces the one-ciphertext kernels
+    const char *v1 = getenv("TAE_BR_V1");
+    batched512_ = p_.N == 512 && p_.k == 4 && !(v1 && v1[0] == '1');
+    const int w16e[5] = {1, 2, 3, 6, 9};
+    for (int i = 0; i < 5; i++) {
+        w16_[2 * i] = t.w[2 * (w16e[i] * t.M / 16)];
+        w16_[2 * i + 1] = t.w[2 * (w16e[i] * t.M / 16) + 1];
+    }
+    if (batched512_) {
+        HIPC(hipFuncSetAttribute((const void *)br512::br_kernel<kBrC, 3, true>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        HIPC(hipFuncSetAttribute((const void *)br512::br_kernel<kBrC, 1, false>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    }
     // opt-in to >64 KiB dynamic LDS for the blind-rotation kernels
     if (p_.N == 512) {
         HIPC(hipFuncSetAttribute((const void *)pbs_kernel<512>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -552,6 +579,14 @@ void Engine::keyswitch(const uint64_t *d_in, uint64_t *d_out, size_t B) {
 void Engine::bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint64_t *d_big, size_t B,
                        uint64_t body_add, uint64_t out_add) {
     if (!B) return;
+    if (batched512_ && p_.pbs_l == 3) {
+        const br512::W16 W = make_w16(w16_);
+        const size_t wgs = (B + kBrC - 1) / kBrC;
+        br512::br_kernel<kBrC, 3, true><<<(unsigned)wgs, kThreads, br512::lds_bytes(kBrC), stream_>>>(
+            d_small, p_.n, d_lut_glwe, 0, d_bsk_f_, 0, d_big, (long)B, p_.pbs_b, body_add, out_add, d_twist_, d_w_, W);
+        HIPC(hipGetLastError());
+        return;
+    }
     for (size_t off = 0; off < B; off += 65535) {
         const unsigned g = (unsigned)std::min<size_t>(65535, B - off);
         if (p_.N == 512) {
@@ -603,6 +638,14 @@ void Engine::vertical_packing(const cplx *d_ggsw_f, size_t G, int n_in, const ui
     int logN = 0;
     while ((1 << logN) < p_.N) logN++;
     if (n_in > logN) throw std::runtime_error("vertical packing with a CMux tree (input_bits > log2 N) is not supported on device");
+    if (batched512_ && p_.cbs_l == 1) {
+        const br512::W16 W = make_w16(w16_);
+        const size_t wgs = G * (size_t)((n_out + kBrC - 1) / kBrC);
+        br512::br_kernel<kBrC, 1, false><<<(unsigned)wgs, kThreads, br512::lds_bytes(kBrC), stream_>>>(
+            nullptr, 0, d_lut, n_out, d_ggsw_f, n_in, d_out, (long)G, p_.cbs_b, 0, 0, d_twist_, d_w_, W);
+        HIPC(hipGetLastError());
+        return;
+    }
     const size_t total = G * (size_t)n_out;
     for (size_t off = 0; off < total; off += 65535 - (65535 % n_out)) {
         const size_t chunk = std::min<size_t>(65535 - (65535 % n_out), total - off);
