@@ -31,6 +31,7 @@ README_KEY = bytes.fromhex("76b8e0ada0f13d90405d6ae55386bd28")  # README / main.
 README_IV = bytes.fromhex("bdd219b8a08ded1a")
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (= FP64 matrix) dense peak, spec
+PBS_KERNEL = "tae::br512::br_kernel<3, 3, true>"
 
 
 def pbs_algorithmic(p, bits):
@@ -62,6 +63,7 @@ def main():
     import torch  # plumbing: device memory + torch.distributed (nccl == RCCL)
     import tfhe_aes
     from tfhe_aes import aes_128
+    from tfhe_aes import distributed as D
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -91,14 +93,7 @@ def main():
         from tfhe_aes import _native as N
         lens = [C.c_size_t() for _ in range(3)]
         N.check(N.lib().tae_server_key_sizes(pid, *[C.byref(x) for x in lens]))
-        bufs = []
-        for i, n in enumerate(lens):
-            if rank == 0:
-                tt = torch.from_numpy(raw[i].view(np.int64)).to(f"cuda:{dev}")
-            else:
-                tt = torch.empty(n.value, dtype=torch.int64, device=f"cuda:{dev}")
-            dist.broadcast(tt, src=0)
-            bufs.append(tt)
+        bufs = D.broadcast_u64(dist, raw if rank == 0 else None, [x.value for x in lens], rank, f"cuda:{dev}")
         torch.cuda.synchronize()
         ctx = tfhe_aes.context_from_raw(pid, [b.data_ptr() for b in bufs], device=dev, mem=1)
         ctx._keepalive = bufs
@@ -127,11 +122,10 @@ def main():
 
     # ---- this rank's counter blocks (main.rs:108-115), encrypted client side, resident in HBM ----
     nb = args.blocks_per_gpu
-    ctrs = range(rank * nb + 1, (rank + 1) * nb + 1)
-    blocks = [README_IV + c.to_bytes(8, "big") for c in ctrs]
+    blocks = D.counter_blocks_for_rank(README_IV, rank, world, nb)
     t = time.time()
     bits = aes_128.blocks_to_bits(blocks)
-    cts = ck.encrypt_bits_raw(bits, start_index=(1 << 32) + rank * nb * 128)
+    cts = ck.encrypt_bits_raw(bits, start_index=D.encrypt_start_index(rank, nb))
     encrypt_s = time.time() - t
     blk_dev = torch.from_numpy(cts.view(np.int64)).to(f"cuda:{dev}")
     out_dev = torch.empty_like(blk_dev)
@@ -161,9 +155,7 @@ def main():
     elapsed = time.time() - t0
     ctx.set_timing(False)
     if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        elapsed = D.max_over_ranks(dist, elapsed, f"cuda:{dev}")
 
     # ---- correctness gate: decrypt and compare with plain AES (outside the timed region) ----
     out = out_dev.cpu().numpy().view(np.uint64)
@@ -171,9 +163,7 @@ def main():
     ek_plain = aes_128.key_schedule_plain(README_KEY)
     ok = int(all(g == aes_128.encrypt_block_plain(ek_plain, b, args.rounds) for g, b in zip(got, blocks)))
     if dist:
-        tt = torch.tensor([ok], dtype=torch.int32, device=f"cuda:{dev}")
-        dist.all_reduce(tt, op=dist.ReduceOp.MIN)
-        ok = int(tt.item())
+        ok = D.min_over_ranks(dist, ok, f"cuda:{dev}")
     if not ok:
         raise SystemExit(f"rank {rank}: decrypted AES output differs from plain AES")
 
@@ -187,20 +177,26 @@ def main():
     bytes_launch, flop_launch = pbs_algorithmic(p, nb * 16 * 8)
     gbs = bytes_launch / (pbs_ms * 1e-3) / 1e9 if pbs_ms > 0 else None
     tflops = flop_launch / (pbs_ms * 1e-3) / 1e12 if pbs_ms > 0 else None
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_pbs_latest.json")
+    # HBM traffic per launch of the same kernel from the committed PMC pass (scripts/bench_profile.sh
+    # -> scripts/prof_summary.py: 2 x FETCH_SIZE + WRITE_SIZE), valid only for the same batch shape.
+    traffic, traffic_src = None, None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if os.path.exists(pmc_path):
         with open(pmc_path) as fh:
             pm = json.load(fh)
-        if pm.get("bits_per_launch") == nb * 16 * 8:
-            traffic = pm.get("hbm_bytes_per_launch")
-    roofline = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": (gbs / HBM_PEAK_GBS) if gbs else None, "traffic": traffic,
-                "kernel": "pbs_kernel<512> (homomorphic_shift_boolean)", "avg_launch_ms": pbs_ms,
-                "algorithmic_bytes_per_launch": bytes_launch,
-                "fp64": {"achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": (tflops / FP64_PEAK_TFLOPS) if tflops else None,
-                         "algorithmic_flop_per_launch": flop_launch}}
+        ent = pm.get("kernels", {}).get(PBS_KERNEL, {})
+        if pm.get("blocks_per_gpu") == nb and "hbm_bytes_per_launch" in ent:
+            traffic, traffic_src = ent["hbm_bytes_per_launch"], pm.get("source")
+    # The batched blind rotation is FP64-bound (>= 10 flop/B at any batch); its roofline
+    # is the chip's dense f64 peak (MFMA and VALU alike on MI355X), HBM figures ride along.
+    roofline = {"bound": "mfma", "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": (tflops / FP64_PEAK_TFLOPS) if tflops else None, "traffic": traffic,
+                "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
+                "kernel": PBS_KERNEL + " (homomorphic_shift_boolean blind rotation)", "avg_launch_ms": pbs_ms,
+                "algorithmic_flop_per_launch": flop_launch,
+                "hbm": {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": (gbs / HBM_PEAK_GBS) if gbs else None,
+                        "algorithmic_bytes_per_launch": bytes_launch}}
     stage_share = {k: v / args.steps for k, v in stage_ms.items()}
 
     cpu = None
@@ -211,7 +207,7 @@ def main():
     if rank == 0:
         rec = {"metric": "FHE AES-128 blocks/sec", "value": value, "unit": "blocks/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": "u64 torus / f64 FFT", "data": "synthetic",
+               "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
                "config": {"workload": f"{nb} counter-mode blocks per GPU, 10-round FHE AES-128 "
                                       "(ShortintWoppbs1BitSboxGalMulPbsAesEncrypt, params_sqrd_lvl_64)",
                           "blocks_per_gpu": nb, "global_blocks": nb * world, "rounds": args.rounds,
@@ -225,7 +221,7 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(raw, ck, threads):
+def cpu_baseline(raw, ck, threads, min_s=10.0):
     """CPU oracle (restatement, kind "port") on a bounded sample of the same workload: the 16 SBOX
     circuit bootstraps of one AES round of one block, threads over bytes as the reference's rayon
     (fhe_sbox_gal_mul_pbs.rs:33-41); blocks/s = 1 / (10 x round time)."""
@@ -234,12 +230,16 @@ def cpu_baseline(raw, ck, threads):
     ok = oracle.Keys(oracle.PARAMS_SQRD_LVL_64, None, raw=raw)
     blk = README_IV + (1).to_bytes(8, "big")
     cts = ck.encrypt_bits_raw(aes_128.blocks_to_bits([blk]), start_index=7 << 40)
-    t = time.time()
-    ok.sub_bytes_gal_mul(cts, threads)
-    dt = time.time() - t
-    return {"value": 1.0 / (10 * dt), "unit": "blocks/s", "cores": threads, "kind": "port",
-            "sample": f"16 SBOX 8->24 circuit bootstraps (one AES round of one block) on {threads} threads "
-                      f"in {dt:.2f} s, x10 rounds"}
+    reps, t = 0, time.time()
+    while True:  # bounded sample: whole rounds of 16 SBOX until >= min_s of CPU work
+        ok.sub_bytes_gal_mul(cts, threads)
+        reps += 1
+        dt = time.time() - t
+        if dt >= min_s:
+            break
+    return {"value": reps / (10 * dt), "unit": "blocks/s", "cores": threads, "kind": "port",
+            "sample": f"{reps} x 16 SBOX 8->24 circuit bootstraps (one AES round of one block each) on "
+                      f"{threads} threads in {dt:.2f} s; blocks/s = rounds/s / 10"}
 
 
 if __name__ == "__main__":

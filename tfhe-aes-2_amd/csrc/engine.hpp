@@ -108,6 +108,12 @@ class Engine {
     cplx *d_ggsw_f_ = nullptr;
     size_t cap_small_ = 0, cap_big_ = 0, cap_ggsw_ = 0, cap_ggsw_f_ = 0, cap_state_ = 0, cap_muls_ = 0;
     hipEvent_t ev_[8];
+    // int8 MFMA keyswitches (ksgemm.hpp): key limb matrices + digit scratch
+    bool mfma_ks_ = false;
+    int8_t *d_pf_bt_ = nullptr, *d_ks_bt_ = nullptr, *d_digits_ = nullptr;
+    size_t cap_digits_ = 0;
+    int kp_pf_ = 0, kp_ks_ = 0;
+    void prepare_mfma_keys();
     double w16_[10] = {};     // W_16^{1,2,3,6,9} from the FFT table (batched N=512 kernels)
     bool batched512_ = false; // N == 512, k == 4: multi-ciphertext blind-rotation kernels
     bool timing_ = false;

@@ -18,6 +18,7 @@
 
 #include "aes.hpp"
 #include "br512.hpp"
+#include "ksgemm.hpp"
 #include "engine.hpp"
 #include "fft_device.hpp"
 
@@ -532,6 +533,42 @@ Engine::Engine(const ServerKeyRaw &keys, int device) : p_(keys.p), device_(devic
     HIPC(hipMemcpy(d_bsk, keys.bsk.data(), keys.bsk.size() * 8, hipMemcpyHostToDevice));
     bsk_to_fourier(d_bsk);
     HIPC(hipFree(d_bsk));
+    prepare_mfma_keys();
+}
+
+// Key limb matrices for the int8-MFMA keyswitches (ksgemm.hpp), built once on device.
+void Engine::prepare_mfma_keys() {
+    const char *v = getenv("TAE_KS_VALU");
+    mfma_ks_ = !(v && v[0] == '1') && p_.pfks_b * 1 <= 16 && p_.ks_b <= 7;
+    if (!mfma_ks_) return;
+    const int glwe = (int)p_.glwe_len();
+    const int kd_pf = (p_.K() + 1) * p_.pfks_l, kd_ks = p_.K() * p_.ks_l;
+    kp_pf_ = (kd_pf + ksgemm::TK - 1) / ksgemm::TK * ksgemm::TK;
+    kp_ks_ = (kd_ks + ksgemm::TK - 1) / ksgemm::TK * ksgemm::TK;
+    const int nc_pf = (p_.k + 1) * glwe, nc_ks = p_.n + 1;
+    d_pf_bt_ = static_cast<int8_t *>(alloc((size_t)nc_pf * 8 * kp_pf_));
+    d_ks_bt_ = static_cast<int8_t *>(alloc((size_t)nc_ks * 8 * kp_ks_));
+    dim3 gpf((kp_pf_ + 63) / 64, (nc_pf + 63) / 64), gks((kp_ks_ + 63) / 64, (nc_ks + 63) / 64);
+    ksgemm::prep_key<<<gpf, kThreads, 0, stream_>>>(d_pfpksk_, d_pf_bt_, kd_pf, kp_pf_, nc_pf, glwe, glwe,
+                                                    (long)(p_.K() + 1) * p_.pfks_l * glwe);
+    ksgemm::prep_key<<<gks, kThreads, 0, stream_>>>(d_ksk_, d_ks_bt_, kd_ks, kp_ks_, nc_ks, nc_ks, nc_ks, 0);
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(stream_));
+}
+
+// digit scratch for B ciphertexts x rows_per_ct rows of Kp bytes (padding columns zeroed)
+static void ensure_digits(int8_t *&buf, size_t &cap, size_t rows, int Kd, int Kp, hipStream_t s) {
+    const size_t need = rows * (size_t)Kp;
+    if (need > cap) {
+        if (buf) hip_check(hipFree(buf), "hipFree");
+        hip_check(hipMalloc(&buf, need), "hipMalloc digits");
+        cap = need;
+    }
+    if (Kp > Kd) {
+        const size_t total = rows * (size_t)(Kp - Kd);
+        ksgemm::zero_pad<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(buf, (long)rows, Kd, Kp);
+        hip_check(hipGetLastError(), "zero_pad");
+    }
 }
 
 Engine::Engine(const Params &p, int device, const uint64_t *d_ksk, const uint64_t *d_bsk,
@@ -542,6 +579,7 @@ Engine::Engine(const Params &p, int device, const uint64_t *d_ksk, const uint64_
     d_ksk_ = const_cast<uint64_t *>(d_ksk);
     d_pfpksk_ = const_cast<uint64_t *>(d_pfpksk);
     bsk_to_fourier(d_bsk);
+    prepare_mfma_keys();
 }
 
 Engine::~Engine() {
@@ -553,7 +591,8 @@ Engine::~Engine() {
     }
     for (void *q : {(void *)d_bsk_f_, (void *)d_twist_, (void *)d_untwist_, (void *)d_w_, (void *)d_lut_shift_,
                     (void *)d_lut24_, (void *)d_lut8_, (void *)d_small_, (void *)d_big_, (void *)d_ggsw_,
-                    (void *)d_ggsw_f_, (void *)d_state_, (void *)d_muls_})
+                    (void *)d_ggsw_f_, (void *)d_state_, (void *)d_muls_, (void *)d_pf_bt_, (void *)d_ks_bt_,
+                    (void *)d_digits_})
         if (q) hipFree(q);
     for (auto &e : ev_) hipEventDestroy(e);
     hipStreamDestroy(stream_);
@@ -571,6 +610,19 @@ void Engine::reserve(size_t bits, size_t outputs) {
 
 void Engine::keyswitch(const uint64_t *d_in, uint64_t *d_out, size_t B) {
     if (!B) return;
+    if (mfma_ks_) {
+        const int K = p_.K(), kd = K * p_.ks_l;
+        ensure_digits(d_digits_, cap_digits_, B, kd, kp_ks_, stream_);
+        const size_t thr = B * (size_t)K;
+        ksgemm::prep_digits<1, 8><<<(unsigned)((thr + 255) / 256), 256, 0, stream_>>>(
+            d_in, K + 1, d_digits_, (long)B, K, kp_ks_, p_.ks_b, p_.ks_l);
+        const long mtiles = (long)((B + ksgemm::TM - 1) / ksgemm::TM);
+        const long ntiles = ((long)(p_.n + 1) * 8 + ksgemm::TN - 1) / ksgemm::TN;
+        ksgemm::gemm<1, 8><<<(unsigned)(mtiles * ntiles), 256, 0, stream_>>>(
+            d_digits_, d_ks_bt_, kp_ks_, (long)B, mtiles, p_.n + 1, d_out, p_.n + 1, (long)B, d_in + K, K + 1, p_.n);
+        HIPC(hipGetLastError());
+        return;
+    }
     dim3 grid((unsigned)((p_.n + 1 + kThreads - 1) / kThreads), (unsigned)((B + KS_CT - 1) / KS_CT));
     keyswitch_kernel<<<grid, kThreads, 0, stream_>>>(d_in, d_out, d_ksk_, B, p_.K(), p_.n, p_.ks_l, p_.ks_b);
     HIPC(hipGetLastError());
@@ -610,6 +662,23 @@ void Engine::pbs_shift_boolean(const uint64_t *d_small, uint64_t *d_big, size_t 
 void Engine::pfks_into_ggsw(const uint64_t *d_big, uint64_t *d_ggsw, size_t B, int level) {
     if (!B) return;
     const int glwe = (int)p_.glwe_len();
+    if (mfma_ks_) {
+        constexpr int MA = 4, LB = 5;  // 17-bit signed digits as 4 balanced 5-bit limbs
+        const int K = p_.K(), kd = (K + 1) * p_.pfks_l;
+        ensure_digits(d_digits_, cap_digits_, B * MA, kd, kp_pf_, stream_);
+        const size_t thr = B * (size_t)(K + 1);
+        ksgemm::prep_digits<MA, LB><<<(unsigned)((thr + 255) / 256), 256, 0, stream_>>>(
+            d_big, K + 1, d_digits_, (long)B, K + 1, kp_pf_, p_.pfks_b, p_.pfks_l);
+        const int ncols = (p_.k + 1) * glwe;
+        const long mtiles = (long)((B * MA + ksgemm::TM - 1) / ksgemm::TM);
+        const long ntiles = ((long)ncols * 8 + ksgemm::TN - 1) / ksgemm::TN;
+        const long out_stride = (long)p_.cbs_l * ncols;
+        ksgemm::gemm<MA, LB><<<(unsigned)(mtiles * ntiles), 256, 0, stream_>>>(
+            d_digits_, d_pf_bt_, kp_pf_, (long)B * MA, mtiles, ncols, d_ggsw + (size_t)(level - 1) * ncols, out_stride,
+            (long)B, nullptr, 0, -1);
+        HIPC(hipGetLastError());
+        return;
+    }
     dim3 grid((unsigned)((glwe + kThreads - 1) / kThreads), (unsigned)(p_.k + 1), (unsigned)((B + PF_CT - 1) / PF_CT));
     pfks_kernel<<<grid, kThreads, 0, stream_>>>(d_big, d_ggsw, d_pfpksk_, B, p_.K(), glwe, p_.pfks_l, p_.pfks_b,
                                                 p_.cbs_l, level, p_.k);

@@ -1,0 +1,229 @@
+// Integer keyswitch as an int8 MFMA GEMM (exact mod 2^64).
+//
+// Both keyswitches of the hot path are   out[b][col] = body - sum_{kd} d[b][kd] * KEY[kd][col]
+//   PFKS  (private_functional_keyswitch_lwe_ciphertext_into_glwe_ciphertext, all k+1 keys at once):
+//         kd = (i, l) over the K+1 big-LWE coefficients x pfks_l levels, col = (q, t) over the
+//         (k+1) x (k+1)N GGSW row coefficients, d = signed 2^16-base digits (17-bit range)
+//   KS    (keyswitch_lwe_ciphertext): kd = (i, l) over K x ks_l, col over n+1, |d| <= 4
+// With u64 keys and small signed digits this is a GEMM of (B x Kd) by (Kd x C) modulo 2^64.  It
+// runs on the i8 matrix cores:
+//   KEY = sum_j k_j 256^j      with balanced signed bytes k_j (8 limbs, wraps mod 2^64)
+//   d   = sum_m d_m 2^(LB m)   with balanced signed LB-bit limbs (MA limbs; MA = 1 for KS)
+//   d * KEY = sum_{m,j} 2^(LB m + 8 j) (d_m k_j)  (mod 2^64)
+// The GEMM rows are (b, m) and the columns (col, j); every i32 partial sum is exact
+// (|d_m k_j| <= 2^(LB-1) * 128, summed over <= 2^13 terms), and the epilogue recombines the
+// MA x 8 partial sums of each (b, col): shift, sum over m in-lane, sum over j across 8 lanes.
+// Integer results are therefore bit-identical to the u64 loop of the CPU oracle.
+//
+// Tiling: 256 threads = 4 waves (2 x 2), workgroup tile 128 rows x 128 cols, K tile 128 bytes,
+// v_mfma_i32_32x32x32_i8 (lane l: A[l & 31][16 (l >> 5) + t], B[16 (l >> 5) + t][l & 31];
+// verified by scripts/probes/mfma_i8_layout.hip).  LDS rows padded to 144 B (conflict-free
+// ds_read_b128), double-buffered; m-tiles vary fastest so a key tile is reused from L2.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace tae {
+namespace ksgemm {
+
+constexpr int TM = 128, TN = 128, TK = 128, LROW = TK + 16;
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+// balanced signed byte limbs of a u64 (k = sum_j limb_j 256^j mod 2^64)
+__device__ __forceinline__ void key_limbs(uint64_t k, int8_t *lb) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const int8_t s = (int8_t)(uint8_t)(k & 0xFF);
+        lb[j] = s;
+        k = (k - (uint64_t)(int64_t)s) >> 8;
+    }
+}
+
+// ---- key preparation: u64 key rows -> Bt[(col * 8 + j) * Kp + kd] (int8) ----
+// key element for (kd, col) at key[kd * key_kd_stride + (col / cols_per_block) * key_blk_stride +
+// col % cols_per_block]; used for both PFPKSK ([q][i][l][glwe]) and KSK ([i][l][n+1]).
+__global__ void __launch_bounds__(256) prep_key(const uint64_t *__restrict__ key, int8_t *__restrict__ Bt, int Kd, int Kp,
+                                                int ncols, int cols_per_block, long key_kd_stride,
+                                                long key_blk_stride) {
+    __shared__ int8_t tile[64][8][65];
+    const int kd0 = blockIdx.x * 64, col0 = blockIdx.y * 64;
+    // load 64 kd x 64 cols (col fastest, coalesced), split into limbs
+    for (int t = threadIdx.x; t < 64 * 64; t += 256) {
+        const int kk = t >> 6, cc = t & 63;
+        const int kd = kd0 + kk, col = col0 + cc;
+        int8_t lb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (kd < Kd && col < ncols) {
+            const uint64_t v = key[(long)kd * key_kd_stride + (long)(col / cols_per_block) * key_blk_stride +
+                                   col % cols_per_block];
+            key_limbs(v, lb);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) tile[cc][j][kk] = lb[j];
+    }
+    __syncthreads();
+    // write rows (col, j) with 64 contiguous kd bytes
+    for (int t = threadIdx.x; t < 64 * 8 * 64; t += 256) {
+        const int kk = t & 63, row = t >> 6;  // row = cc * 8 + j
+        const int cc = row >> 3, j = row & 7;
+        const int col = col0 + cc, kd = kd0 + kk;
+        if (col < ncols && kd < Kp) Bt[((long)col * 8 + j) * Kp + kd] = tile[cc][j][kk];
+    }
+}
+
+// ---- digits: big LWE [B][K+1] -> A[(b * MA + m) * Kp + i * L + (lev - 1)] ----
+template <int MA, int LB>
+__global__ void __launch_bounds__(256) prep_digits(const uint64_t *__restrict__ in, long in_stride, int8_t *__restrict__ A,
+                                                   long B, int n_in, int Kp, int base_log, int levels) {
+    const long t = (long)blockIdx.x * 256 + threadIdx.x;
+    const long b = t / n_in;
+    const int i = (int)(t - b * n_in);
+    if (b >= B) return;
+    const uint64_t x = in[b * in_stride + i];
+    // tfhe-rs SignedDecomposer: closest representable, balanced digits (finest first)
+    const int nrb = 64 - base_log * levels;
+    uint64_t s = x >> (nrb - 1);
+    s += s & 1;
+    s >>= 1;
+    const uint64_t mask = (1ull << base_log) - 1;
+    for (int lev = levels; lev >= 1; lev--) {
+        const uint64_t res = s & mask;
+        s >>= base_log;
+        uint64_t carry = ((res - 1) | s) & res;
+        carry >>= (base_log - 1);
+        s += carry;
+        int32_t d = (int32_t)(res - (carry << base_log));
+        const long kd = (long)i * levels + (lev - 1);
+#pragma unroll
+        for (int m = 0; m < MA; m++) {
+            int32_t limb;
+            if (m == MA - 1) {
+                limb = d;
+            } else {
+                limb = ((d + (1 << (LB - 1))) & ((1 << LB) - 1)) - (1 << (LB - 1));
+                d = (d - limb) >> LB;
+            }
+            A[(b * MA + m) * Kp + kd] = (int8_t)limb;
+        }
+    }
+}
+
+// zero the padding columns kd in [Kd, Kp) of every row (done once per buffer size change)
+__global__ void zero_pad(int8_t *A, long rows, int Kd, int Kp) {
+    const long t = (long)blockIdx.x * 256 + threadIdx.x;
+    const int w = Kp - Kd;
+    const long r = t / w;
+    if (r < rows) A[r * Kp + Kd + (int)(t - r * w)] = 0;
+}
+
+// ---- the GEMM ----
+template <int MA, int LB>
+__global__ void __launch_bounds__(256, 2)
+    gemm(const int8_t *__restrict__ A, const int8_t *__restrict__ Bt, int Kp, long Mrows, long mtiles, int ncols,
+         uint64_t *__restrict__ out, long out_stride, long B, const uint64_t *__restrict__ body_in, long body_stride,
+         int body_col) {
+    __shared__ __align__(16) int8_t sA[2][TM * LROW];
+    __shared__ __align__(16) int8_t sB[2][TN * LROW];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int wm = wave >> 1, wn = wave & 1;
+    const long mt = blockIdx.x % mtiles, nt = blockIdx.x / mtiles;
+    const long row0 = mt * TM;
+    const long col8_0 = nt * TN;  // first (col, j) column of the tile
+    const long N8 = (long)ncols * 8;
+
+    // loader mapping: chunk c = tid + 256 t (t < 4): row = c >> 3, 16-byte column kc = c & 7
+    v4i ra[4], rb[4];
+    auto gload = [&](int k0) {
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const int c = tid + 256 * t, r = c >> 3, kc = c & 7;
+            const long ar = row0 + r, br = col8_0 + r;
+            ra[t] = ar < Mrows ? *reinterpret_cast<const v4i *>(A + ar * Kp + k0 + kc * 16) : v4i{0, 0, 0, 0};
+            rb[t] = br < N8 ? *reinterpret_cast<const v4i *>(Bt + br * Kp + k0 + kc * 16) : v4i{0, 0, 0, 0};
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const int c = tid + 256 * t, r = c >> 3, kc = c & 7;
+            *reinterpret_cast<v4i *>(&sA[buf][r * LROW + kc * 16]) = ra[t];
+            *reinterpret_cast<v4i *>(&sB[buf][r * LROW + kc * 16]) = rb[t];
+        }
+    };
+
+    v16i acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++) acc[a][b] = v16i{0};
+
+    const int r = lane & 31, h = lane >> 5;
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    const int nk = Kp / TK;
+    for (int ks = 0; ks < nk; ks++) {
+        const int cur = ks & 1;
+        if (ks + 1 < nk) gload((ks + 1) * TK);
+#pragma unroll
+        for (int kk = 0; kk < TK / 32; kk++) {
+            v4i fa[2], fb[2];
+#pragma unroll
+            for (int ti = 0; ti < 2; ti++)
+                fa[ti] = *reinterpret_cast<const v4i *>(&sA[cur][(wm * 64 + ti * 32 + r) * LROW + kk * 32 + h * 16]);
+#pragma unroll
+            for (int tj = 0; tj < 2; tj++)
+                fb[tj] = *reinterpret_cast<const v4i *>(&sB[cur][(wn * 64 + tj * 32 + r) * LROW + kk * 32 + h * 16]);
+#pragma unroll
+            for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+                for (int tj = 0; tj < 2; tj++)
+                    acc[ti][tj] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[ti], fb[tj], acc[ti][tj], 0, 0, 0);
+        }
+        if (ks + 1 < nk) {
+            lstore(cur ^ 1);
+            __syncthreads();
+        }
+    }
+
+    // ---- epilogue: recombine limbs, reduce over the 8 key limbs, store ----
+    const int j = r & 7;  // key limb of this lane's column
+#pragma unroll
+    for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+        for (int tj = 0; tj < 2; tj++) {
+            const long col = (col8_0 + wn * 64 + tj * 32 + r) >> 3;
+            // rows of reg q: (q & 3) + 8 (q >> 2) + 4 h  within the 32-row tile
+#pragma unroll
+            for (int g = 0; g < 16 / MA; g++) {
+                uint64_t v = 0;
+#pragma unroll
+                for (int m = 0; m < MA; m++) {
+                    const int q = g * MA + m;
+                    const int sh = LB * m + 8 * j;
+                    const uint64_t p = (uint64_t)(int64_t)acc[ti][tj][q];
+                    v += sh < 64 ? (p << sh) : 0;
+                }
+                // sum over the 8 lanes (j = 0..7) that hold the same column
+#pragma unroll
+                for (int x = 1; x < 8; x <<= 1) {
+                    const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+                    const uint32_t olo = __shfl_xor((int)lo, x, 64), ohi = __shfl_xor((int)hi, x, 64);
+                    v += ((uint64_t)ohi << 32) | olo;
+                }
+                const int q0 = g * MA;
+                const int row = (q0 & 3) + 8 * (q0 >> 2) + 4 * h;
+                const long grow = row0 + wm * 64 + ti * 32 + row;  // (b, m=0) row
+                const long b = grow / MA;
+                if (j == 0 && col < ncols && b < B) {
+                    uint64_t o = 0 - v;
+                    if (col == body_col) o += body_in[b * body_stride];
+                    out[b * out_stride + col] = o;
+                }
+            }
+        }
+}
+
+}  // namespace ksgemm
+}  // namespace tae
