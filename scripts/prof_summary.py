@@ -21,7 +21,7 @@ def find(out, sub, pattern):
 
 
 def short(name):
-    return name.split("(")[0].replace("void ", "").strip()
+    return name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").strip()
 
 
 def counters(path):
