@@ -130,15 +130,16 @@ __global__ void __launch_bounds__(256, 1)
     }
     const bool jvalid = fjob && jct < nct;
 
-    // ---- twiddle tables in LDS: twist e^{i pi j/N}; pass-A twiddles laid out per lane,
-    //      s_twa[16 u + k] = W_M^{u k}, so every lane reads them at constant offsets ----
+    // ---- twiddle tables in LDS: twist e^{i pi j/N}; pass-A twiddles s_twa[16 a + b] = W_M^{a b}
+    //      (symmetric), read by lane u at s_twa[16 k + u]: constant offsets, and the 16 lanes of a
+    //      job hit 16 distinct 4-bank groups (the u-major read was a 16-way ds_read_b128 conflict) ----
     cplx *s_tw = buf + JOBS * BUF_STRIDE;
     cplx *s_twa = s_tw + M;
     for (int t = tid; t < M; t += 256) {
         s_tw[t] = twist[t];
         s_twa[t] = wtab[(t >> 4) * (t & 15)];
     }
-    const cplx *my_twa = s_twa + TPJ * u;
+    const cplx *my_twa = s_twa + u;
 
     // ---- GGSW stream through a buffer descriptor: per-lane voffset, uniform soffset ----
     const cplx *gbase = PBS ? ggsw_base : ggsw_base + (size_t)g * n_in * ggsw_sz;
@@ -242,7 +243,7 @@ __global__ void __launch_bounds__(256, 1)
                 dft16<false>(v, W);
                 if (u != 0) {
 #pragma unroll
-                    for (int kk = 1; kk < R; kk++) v[kk] = cmul(v[kk], my_twa[kk]);
+                    for (int kk = 1; kk < R; kk++) v[kk] = cmul(v[kk], my_twa[TPJ * kk]);
                 }
                 cplx *dst = buf + jb * BUF_STRIDE;
 #pragma unroll
@@ -313,7 +314,7 @@ __global__ void __launch_bounds__(256, 1)
             for (int kk = 0; kk < R; kk++) v[kk] = src[pidx(u + TPJ * kk)];
             if (u != 0) {
 #pragma unroll
-                for (int kk = 1; kk < R; kk++) v[kk] = cmul(v[kk], cconj(my_twa[kk]));
+                for (int kk = 1; kk < R; kk++) v[kk] = cmul(v[kk], cconj(my_twa[TPJ * kk]));
             }
             dft16<true>(v, W);
             uint64_t *poly = acc + jb * ACC_STRIDE + uu;  // coefficient j = u + 16 m

@@ -18,7 +18,7 @@
 // Tiling: 256 threads = 4 waves (2 x 2), workgroup tile 128 rows x 128 cols, K tile 128 bytes,
 // v_mfma_i32_32x32x32_i8 (lane l: A[l & 31][16 (l >> 5) + t], B[16 (l >> 5) + t][l & 31];
 // verified by scripts/probes/mfma_i8_layout.hip).  LDS rows padded to 144 B (conflict-free
-// ds_read_b128), double-buffered; m-tiles vary fastest so a key tile is reused from L2.
+// ds_read_b128), double-buffered; grouped tile order (see gemm) bounds the HBM re-reads.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -127,7 +127,15 @@ __global__ void __launch_bounds__(256, 2)
     __shared__ __align__(16) int8_t sB[2][TN * LROW];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int wm = wave >> 1, wn = wave & 1;
-    const long mt = blockIdx.x % mtiles, nt = blockIdx.x / mtiles;
+    // grouped tile order: GN n-tiles per group, n fastest inside it.  The ~512 co-resident WGs
+    // cover 16 m-tiles x GN n-tiles, and with round-robin XCD dispatch each XCD keeps GN/8 key
+    // tiles in its L2 while the digits are re-read once per group instead of once per n-tile.
+    constexpr long GN = 32;
+    const long ntiles = (((long)ncols * 8) + TN - 1) / TN;
+    const long gsz = GN * mtiles;
+    const long ng = blockIdx.x / gsz, rr = blockIdx.x - ng * gsz;
+    const long gw = min(GN, ntiles - ng * GN);
+    const long mt = rr / gw, nt = ng * GN + (rr - (rr / gw) * gw);
     const long row0 = mt * TM;
     const long col8_0 = nt * TN;  // first (col, j) column of the tile
     const long N8 = (long)ncols * 8;

@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtfhe_aes_amd.so")
+LIB_PATH = os.environ.get("TAE_LIB_PATH") or os.path.join(_HERE, "libtfhe_aes_amd.so")
 
 TAE_OK, TAE_E_NOISE, TAE_E_INDEP, TAE_E_PARAM, TAE_E_HIP, TAE_E_ARG, TAE_E_NODEV = range(7)
 TAE_MEM_HOST, TAE_MEM_DEVICE = 0, 1
