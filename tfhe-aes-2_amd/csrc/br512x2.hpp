@@ -21,7 +21,6 @@
 namespace tae {
 namespace br512x2 {
 
-using br512::ACC_STRIDE;
 using br512::BUF_STRIDE;
 using br512::K1;
 using br512::lds_sync;
@@ -32,6 +31,38 @@ using br512::u32x4;
 using br512::W16;
 
 constexpr int C = 3, JOBS = C * K1, THREADS = 512;
+
+// A job's 32 lanes live in one wave and LDS operations of a wave execute in order, so hand-offs
+// inside a job (pass A -> pass B, pass B^-1 -> pass A^-1, ACC update -> next decomposition) only
+// need the compiler not to reorder the accesses; workgroup barriers remain where data crosses jobs
+// (spectra -> MAC -> next level / inverse).
+__device__ __forceinline__ void wave_sync() { asm volatile("" ::: "memory"); }
+constexpr int ACC_STRIDE = N;  // u64 per ACC polynomial (no padding: see acc_phys)
+
+// ACC coefficient j lives at acc_phys(j): bit 5 of j flips bit 4.  The two lanes of a pair touch
+// coefficients 32 apart (same ds_read_b64 bank otherwise); after the swizzle they are 16 u64 =
+// 32 banks apart, and any 16 consecutive coefficients still cover 16 distinct bank pairs.
+__device__ __forceinline__ int acc_phys(int j) { return j ^ ((j & 32) >> 1); }
+
+// coefficient j of poly * X^e (e in [0, 2N)) on a swizzled ACC polynomial
+__device__ __forceinline__ uint64_t rotated_acc(const uint64_t *poly, int j, int e) {
+    int src = j - e;
+    bool neg = false;
+    if (src < 0) {
+        src += N;
+        neg = !neg;
+    }
+    if (src < 0) {
+        src += N;
+        neg = !neg;
+    }
+    const uint64_t v = poly[acc_phys(src)];
+    return neg ? (0 - v) : v;
+}
+
+// MAC thread -> Fourier position: odd 16-blocks rotated by one so that, with the +1-per-16 buffer
+// padding, the 16 lanes of every ds_read_b128 lane group hit 16 distinct 4-bank groups.
+__device__ __forceinline__ int mac_pos(int t) { return (t & 0xF0) | ((t - ((t >> 4) & 1)) & 15); }
 
 __device__ __forceinline__ void swap16(cplx &x, cplx &y) {
     // v_permlane16_swap: lanes of even rows keep x and receive the odd-row partner's x in y;
@@ -100,7 +131,6 @@ __device__ __forceinline__ void mac_level(const cplx *buf, int pos, cplx *accr, 
             im = fma(x[c].im, gg.re, im);
             accr[a] = {re, im};
         }
-        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -157,7 +187,7 @@ __global__ void __launch_bounds__(THREADS, 1)
     const cplx *gbase = PBS ? ggsw_base : ggsw_base + (size_t)g * n_in * ggsw_sz;
     const uint32_t gbytes = (uint32_t)((size_t)(PBS ? n : n_in) * ggsw_sz * sizeof(cplx));
     const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc((void *)gbase, (short)0, gbytes, 0x00020000);
-    const int pos = tid & (M - 1);
+    const int pos = mac_pos(tid & (M - 1));
     const int half = __builtin_amdgcn_readfirstlane(tid >> 8);  // wave-uniform MAC half
     const int gvoff = pos * (int)sizeof(cplx);
 
@@ -175,7 +205,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                 v = c < K1 - 1 ? 0 : lut[(size_t)(ct0 + ct) * N + j];
             }
         }
-        acc[job * ACC_STRIDE + j] = v;
+        acc[job * ACC_STRIDE + acc_phys(j)] = v;
     }
     lds_sync();
 
@@ -216,8 +246,8 @@ __global__ void __launch_bounds__(THREADS, 1)
 #pragma unroll
             for (int L = 0; L < 8; L++) {
                 const int j = uu + 16 * (2 * h + in_idx(L));
-                const uint64_t x0 = rotated_coeff(poly, j, e, N) - poly[j];
-                const uint64_t x1 = rotated_coeff(poly, j + M, e, N) - poly[j + M];
+                const uint64_t x0 = rotated_acc(poly, j, e) - poly[acc_phys(j)];
+                const uint64_t x1 = rotated_acc(poly, j + M, e) - poly[acc_phys(j) + M];
                 int32_t d0[LEV], d1[LEV];
                 br512::decompose_all<LEV>(x0, base_log, d0);
                 br512::decompose_all<LEV>(x1, base_log, d1);
@@ -253,7 +283,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                     dst[pidx(uu + 16 * k)] = cmul(v[S], (s_twa + uu)[16 * k]);
                 }
             }
-            lds_sync();
+            wave_sync();
             // pass B: half DFT16 over positions 16 u + m, in place
             if (fjob) {
                 cplx *base = buf + jb * BUF_STRIDE;
@@ -292,7 +322,7 @@ __global__ void __launch_bounds__(THREADS, 1)
 #pragma unroll
             for (int S = 0; S < 8; S++) base[pidx(16 * uu + 2 * h + out_idx(S))] = v[S];
         }
-        lds_sync();
+        wave_sync();
         if (fjob) {  // pass A^-1: conj(W_M^{u kk}), half DFT16, untwist, from_torus, ACC +=
             const cplx *src = buf + jb * BUF_STRIDE;
             cplx v[8];
@@ -302,7 +332,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                 v[L] = cmul(src[pidx(uu + 16 * kk)], cconj((s_twa + uu)[16 * kk]));
             }
             half_dft16<true>(v, my_w16);
-            uint64_t *poly = acc + jb * ACC_STRIDE + uu;
+            uint64_t *poly = acc + jb * ACC_STRIDE;
             const cplx *twp = s_tw + uu;
 #pragma unroll
             for (int S = 0; S < 8; S++) {
@@ -310,19 +340,21 @@ __global__ void __launch_bounds__(THREADS, 1)
                 const cplx tw = twp[16 * m];
                 const cplx ut = {tw.re * 0x1p-8, -tw.im * 0x1p-8};
                 const cplx t = cmul(v[S], ut);
-                poly[16 * m] += from_torus(t.re);
-                poly[16 * m + M] += from_torus(t.im);
+                const int jp = acc_phys(uu + 16 * m);
+                poly[jp] += from_torus(t.re);
+                poly[jp + M] += from_torus(t.im);
             }
         }
-        lds_sync();
+        wave_sync();
     }
+    lds_sync();  // sample extraction reads every job's ACC
     for (int ct = 0; ct < nct; ct++) {
         const uint64_t *a = acc + ct * K1 * ACC_STRIDE;
         uint64_t *o = PBS ? out + (size_t)(ct0 + ct) * (K1 - 1) * N + (size_t)(ct0 + ct)
                           : out + ((size_t)g * n_out + ct0 + ct) * ((K1 - 1) * N + 1);
         for (int t = tid; t < (K1 - 1) * N; t += THREADS) {
             const int p = t / N, j = t - p * N;
-            o[t] = j == 0 ? a[p * ACC_STRIDE] : (0 - a[p * ACC_STRIDE + N - j]);
+            o[t] = j == 0 ? a[p * ACC_STRIDE] : (0 - a[p * ACC_STRIDE + acc_phys(N - j)]);
         }
         if (tid == 0) o[(K1 - 1) * N] = a[(K1 - 1) * ACC_STRIDE] + out_add;
     }
