@@ -1,0 +1,86 @@
+// Host-side check of the integer-only torus helpers the blind-rotation kernels use
+// (fft_device.hpp: from_torus_bits, decompose16) against the CPU oracle's restatement of tfhe-rs
+// (or_from_torus, or_decompose), on random and edge-case inputs. Built and run by
+// tests/test_native_helpers.py (CPU only).
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <random>
+
+#include "../../tfhe-aes-2_amd/csrc/fft_device.hpp"
+
+extern "C" {
+uint64_t or_from_torus(double x);
+void or_decompose(uint64_t x, int base_log, int levels, int64_t *digits);
+}
+
+static int fails = 0;
+
+static void check_ft(double x) {
+    const uint64_t a = tae::from_torus_bits(x), b = or_from_torus(x);
+    if (a != b && fails++ < 10) printf("from_torus(%a): got %016llx want %016llx\n", x, (unsigned long long)a, (unsigned long long)b);
+}
+
+template <int LEV>
+static void check_dec(uint64_t x, int B) {
+    uint32_t d[LEV];
+    int64_t r[LEV];
+    tae::decompose16<LEV>(x, B, d);
+    or_decompose(x, B, LEV, r);
+    for (int l = 0; l < LEV; l++) {
+        const int64_t got = (int16_t)(d[l] & 0xFFFF);
+        if ((got != r[l] || (d[l] >> 16) != 0) && fails++ < 10)
+            printf("decompose(%016llx, B=%d, L=%d) level %d: got %lld want %lld\n", (unsigned long long)x, B, LEV, l + 1,
+                   (long long)got, (long long)r[l]);
+    }
+}
+
+int main(int argc, char **argv) {
+    const long n = argc > 1 ? atol(argv[1]) : 2000000;
+    std::mt19937_64 rng(12345);
+    // from_torus: magnitudes across every exponent that matters, exact halves, integers, zeros
+    const double specials[] = {0.0, -0.0, 0.5, -0.5, 1.5, -1.5, 2.5, -2.5, 1.0, -1.0, 0x1p-64, -0x1p-64, 0x1p-65,
+                               -0x1p-65, 0x1.8p-65, -0x1.8p-65, 0x1p-66, 0x1p52, -0x1p52, 0x1p53 + 2, 0x1p70, -0x1p70,
+                               0x1p-1022, 0x1p-1074, 1e300, -1e300, 0.25, -0.25, 0x1.fffffffffffffp-2, -0x1.fffffffffffffp-2};
+    for (double x : specials) check_ft(x);
+    for (long i = 0; i < n; i++) {
+        const uint64_t r = rng();
+        const int ex = (int)(r % 100) - 75;  // |x| in [2^-75, 2^25)
+        double x = std::ldexp((double)(rng() >> 11) * 0x1p-53, ex);
+        if (r & (1ull << 40)) x = -x;
+        check_ft(x);
+        // exact halves at random integers and tiny values with ties below 2^-64
+        if ((i & 15) == 0) {
+            const double h = (double)(int64_t)(rng() % 100000) + 0.5;
+            check_ft(h);
+            check_ft(-h);
+            const double t = std::ldexp((double)(2 * (rng() % 1000) + 1), -65 - (int)(rng() % 4));
+            check_ft(t);
+            check_ft(-t);
+        }
+    }
+    // decompositions used by the kernels: PBS (B=12, L=3), CBS / VP (B=13, L=1), 8-bit set (B=7, L=6),
+    // (B=6, L=4), plus edges around the rounding point and the top of the range
+    const uint64_t edges[] = {0, 1, ~0ull, 1ull << 63, (1ull << 63) - 1, (1ull << 27), (1ull << 27) - 1, (1ull << 28) - 1,
+                              0xFFFFFFFFF8000000ull, 0xFFFFFFFFF7FFFFFFull, 0x8008008000000000ull, 0x7FF7FF8000000000ull};
+    for (uint64_t x : edges) {
+        check_dec<3>(x, 12);
+        check_dec<1>(x, 13);
+        check_dec<6>(x, 5);
+        check_dec<4>(x, 6);
+        check_dec<2>(x, 15);
+    }
+    for (long i = 0; i < n; i++) {
+        uint64_t x = rng();
+        if (i & 1) x = (x & ~((1ull << 40) - 1)) | ((uint64_t)(rng() % 5) << 26);  // near-tie digits
+        if ((i & 7) == 0) x = (x & 0xFFFFFFF000000000ull) | (0x800800800ull << 28 >> 28 << 28);
+        check_dec<3>(x, 12);
+        check_dec<1>(x, 13);
+        check_dec<6>(x, 5);
+        check_dec<4>(x, 6);
+        check_dec<2>(x, 15);
+    }
+    printf("%s (%d mismatches)\n", fails ? "FAIL" : "OK", fails);
+    return fails ? 1 : 0;
+}

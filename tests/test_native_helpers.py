@@ -1,0 +1,19 @@
+"""The integer-only torus helpers of the blind-rotation kernels (fft_device.hpp from_torus_bits,
+decompose16), compiled for the host and compared with the CPU oracle's tfhe-rs restatement
+(or_from_torus, or_decompose) on random and edge-case inputs (tests/native/torus_helpers_test.cpp)."""
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_torus_helpers_match_oracle(tmp_path):
+    exe = str(tmp_path / "torus_helpers_test")
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "-ffp-contract=off", "--offload-arch=gfx950",
+                    os.path.join(ROOT, "tests", "native", "torus_helpers_test.cpp"), "-x", "none",
+                    os.path.join(ROOT, "oracle", "build", "liboracle.so"), "-o", exe,
+                    "-Wl,-rpath," + os.path.join(ROOT, "oracle", "build")], check=True)
+    r = subprocess.run([exe, "1000000"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "OK" in r.stdout

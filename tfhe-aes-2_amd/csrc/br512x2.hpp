@@ -37,7 +37,12 @@ constexpr int C = 3, JOBS = C * K1, THREADS = 512;
 // need the compiler not to reorder the accesses; workgroup barriers remain where data crosses jobs
 // (spectra -> MAC -> next level / inverse).
 __device__ __forceinline__ void wave_sync() { asm volatile("" ::: "memory"); }
-constexpr int ACC_STRIDE = N;  // u64 per ACC polynomial (no padding: see acc_phys)
+constexpr int ACC_STRIDE = N;
+#ifdef TAE_DBG_NOBAR
+#define DBG_SYNC() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+#else
+#define DBG_SYNC() lds_sync()
+#endif  // u64 per ACC polynomial (no padding: see acc_phys)
 
 // ACC coefficient j lives at acc_phys(j): bit 5 of j flips bit 4.  The two lanes of a pair touch
 // coefficients 32 apart (same ds_read_b64 bank otherwise); after the swizzle they are 16 u64 =
@@ -136,7 +141,9 @@ __device__ __forceinline__ void mac_level(const cplx *buf, int pos, cplx *accr, 
 
 // Mode: PBS -> GGSW_i = bsk + i * ggsw_sz, per-ciphertext rotation a~_i; steps = n.
 //       VP  -> GGSW_t = ggsw_f + (g * n_in + b) * ggsw_sz, rotation X^{-2^t} shared; steps = n_in.
-template <int LEV, bool PBS>
+// BLOG: decomposition base log (12 for the PBS, 13 for the CBS GGSW of params_sqrd_lvl_64), a
+// template parameter so the digit extraction compiles to constant shifts.
+template <int LEV, bool PBS, int BLOG>
 __global__ void __launch_bounds__(THREADS, 1)
     br_kernel(const uint64_t *__restrict__ lwe_in, int n, const uint64_t *__restrict__ lut, int n_out,
               const cplx *__restrict__ ggsw_base, int n_in, uint64_t *__restrict__ out, long B, int base_log,
@@ -148,7 +155,8 @@ __global__ void __launch_bounds__(THREADS, 1)
     cplx *buf = reinterpret_cast<cplx *>(acc + JOBS * ACC_STRIDE);  // [JOBS][BUF_STRIDE]
     cplx *s_tw = buf + JOBS * BUF_STRIDE;                           // twist e^{i pi j / N}
     cplx *s_twa = s_tw + M;                                         // [16 a + b] = W_M^{a b}
-    cplx *s_w16 = s_twa + M;                                        // [h][6] stage-1 factors
+    cplx *s_utw = s_twa + M;                                        // conj(twist) 2^-8 (exact)
+    cplx *s_w16 = s_utw + M;                                        // [h][6] stage-1 factors
     const int tid = threadIdx.x;
     const int jb = tid >> 5, t32 = tid & 31;
     const int h = t32 >> 4, u = t32 & 15;  // lane pair (u, u + 16) of a job
@@ -172,6 +180,7 @@ __global__ void __launch_bounds__(THREADS, 1)
     for (int t = tid; t < M; t += THREADS) {
         s_tw[t] = twist[t];
         s_twa[t] = wtab[(t >> 4) * (t & 15)];
+        s_utw[t] = cplx{twist[t].re * 0x1p-8, -twist[t].im * 0x1p-8};
     }
     if (tid < 12) {
         // s_w16[6 h + 3 al + b - 1] = W16^{(2h + al) b} = W_M^{16 e}; exact 1 and -i for e = 0, 4.
@@ -241,18 +250,39 @@ __global__ void __launch_bounds__(THREADS, 1)
         int uu = u;
         asm volatile("" : "+v"(uu));
         uint32_t dig[LEV][8];
+#ifdef TAE_DBG_NODEC
         if (fjob) {
             const uint64_t *poly = acc + jb * ACC_STRIDE;
 #pragma unroll
+            for (int L = 0; L < 8; L++)
+#pragma unroll
+                for (int l = 0; l < LEV; l++) dig[l][L] = (uint32_t)poly[acc_phys(uu + 16 * L + l)] ^ e;
+        }
+        if (false) {
+#else
+        if (fjob) {
+#endif
+            const uint64_t *poly = acc + jb * ACC_STRIDE;
+            // coefficient j of ACC * X^e is entry t = (j - e) mod 2N of the negacyclic extension
+            // [ACC, -ACC]: ACC[t mod N], negated when t >= N; coefficient j + M is entry t + M,
+            // stored at phys(t mod N) ^ M (the swizzle leaves bit 8 alone)
+            const int bt = uu + 32 * h - e;
+#pragma unroll
             for (int L = 0; L < 8; L++) {
                 const int j = uu + 16 * (2 * h + in_idx(L));
-                const uint64_t x0 = rotated_acc(poly, j, e) - poly[acc_phys(j)];
-                const uint64_t x1 = rotated_acc(poly, j + M, e) - poly[acc_phys(j) + M];
-                int32_t d0[LEV], d1[LEV];
-                br512::decompose_all<LEV>(x0, base_log, d0);
-                br512::decompose_all<LEV>(x1, base_log, d1);
+                const int t = (bt + 16 * in_idx(L)) & (2 * N - 1);
+                const int ph = acc_phys(t & (N - 1));
+                const uint64_t m0 = (uint64_t)(int64_t)((t << 22) >> 31);
+                const uint64_t m1 = (uint64_t)(int64_t)(((t + M) << 22) >> 31);
+                const uint64_t v0 = poly[ph], v1 = poly[ph ^ M];
+                const uint64_t p0 = poly[acc_phys(j)], p1 = poly[acc_phys(j) + M];
+                // (v ^ m) - (p + m) = v - p, or -v - p when m = -1
+                const uint64_t x0 = (v0 ^ m0) - (p0 + m0), x1 = (v1 ^ m1) - (p1 + m1);
+                uint32_t d0[LEV], d1[LEV];
+                decompose16<LEV>(x0, BLOG, d0);
+                decompose16<LEV>(x1, BLOG, d1);
 #pragma unroll
-                for (int l = 0; l < LEV; l++) dig[l][L] = ((uint32_t)d0[l] & 0xFFFFu) | ((uint32_t)d1[l] << 16);
+                for (int l = 0; l < LEV; l++) dig[l][L] = d0[l] | (d1[l] << 16);
                 if ((L & 3) == 3) __builtin_amdgcn_sched_barrier(0);
             }
         }
@@ -261,7 +291,11 @@ __global__ void __launch_bounds__(THREADS, 1)
 
 #pragma unroll
         for (int lev = LEV; lev >= 1; lev--) {
+#ifndef TAE_DBG_NOGLOAD
             load_level(lev);
+#else
+            if (lev == LEV) load_level(lev);
+#endif
             // pass A: twist, half DFT16 over n2, W_M^{u k}, -> LDS position u + 16 k
             if (fjob) {
                 cplx v[8];
@@ -294,12 +328,14 @@ __global__ void __launch_bounds__(THREADS, 1)
 #pragma unroll
                 for (int S = 0; S < 8; S++) base[pidx(16 * uu + 2 * h + out_idx(S))] = v[S];
             }
-            lds_sync();
+            DBG_SYNC();
+#ifndef TAE_DBG_NOMAC
             if (half == 0)
                 mac_level<0, LEV>(buf, pidx(pos), accr, gv);
             else
                 mac_level<1, LEV>(buf, pidx(pos), accr, gv);
-            lds_sync();
+#endif
+            DBG_SYNC();
         }
         // ---- inverse FFT of the MAC results, accumulated into ACC ----
         {
@@ -312,7 +348,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                 for (int a = 0; a < 7; a++) buf[(((a + 8) % 3) * K1 + (a + 8) / 3) * BUF_STRIDE + pp] = accr[a];
             }
         }
-        lds_sync();
+        DBG_SYNC();
         if (fjob) {  // pass B^-1
             cplx *base = buf + jb * BUF_STRIDE;
             cplx v[8];
@@ -333,16 +369,19 @@ __global__ void __launch_bounds__(THREADS, 1)
             }
             half_dft16<true>(v, my_w16);
             uint64_t *poly = acc + jb * ACC_STRIDE;
-            const cplx *twp = s_tw + uu;
+            const cplx *utp = s_utw + uu;
 #pragma unroll
             for (int S = 0; S < 8; S++) {
                 const int m = 2 * h + out_idx(S);
-                const cplx tw = twp[16 * m];
-                const cplx ut = {tw.re * 0x1p-8, -tw.im * 0x1p-8};
-                const cplx t = cmul(v[S], ut);
+                const cplx t = cmul(v[S], utp[16 * m]);
                 const int jp = acc_phys(uu + 16 * m);
-                poly[jp] += from_torus(t.re);
-                poly[jp + M] += from_torus(t.im);
+#ifdef TAE_DBG_NOTAIL
+                poly[jp] += (uint64_t)__double_as_longlong(t.re);
+                poly[jp + M] += (uint64_t)__double_as_longlong(t.im);
+#else
+                poly[jp] += from_torus_bits(t.re);
+                poly[jp + M] += from_torus_bits(t.im);
+#endif
             }
         }
         wave_sync();
@@ -361,7 +400,7 @@ __global__ void __launch_bounds__(THREADS, 1)
 }
 
 inline size_t lds_bytes() {
-    return (size_t)JOBS * ACC_STRIDE * 8 + (size_t)JOBS * BUF_STRIDE * 16 + 2 * (size_t)M * 16 + 12 * 16;
+    return (size_t)JOBS * ACC_STRIDE * 8 + (size_t)JOBS * BUF_STRIDE * 16 + 3 * (size_t)M * 16 + 12 * 16;
 }
 
 }  // namespace br512x2

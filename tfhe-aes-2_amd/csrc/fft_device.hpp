@@ -125,6 +125,62 @@ __device__ __forceinline__ uint64_t from_torus(double x) {
     return (uint64_t)iv;
 }
 
+__host__ __device__ __forceinline__ uint64_t f64_bits(double x) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return (uint64_t)__double_as_longlong(x);
+#else
+    uint64_t b;
+    __builtin_memcpy(&b, &x, 8);
+    return b;
+#endif
+}
+
+// from_torus on the bits of x, integer ops only; equal to from_torus(x) for every finite x.
+// |x| 2^64 = m 2^s (m the 53-bit significand, s = biased exponent - 1011).
+//   s >= 0: x 2^64 is an integer, f = x - round(x) is exact and f 2^64 == x 2^64 (mod 2^64);
+//   s <  0: |x| < 2^-12 so round(x) = 0 and round(x 2^64) = (m + 2^(k-1)) >> k, k = -s
+//           (half away from zero on the magnitude).
+// The i64 saturation of f 2^64 = +2^63 (x = -(n + 1/2)) gives INT64_MAX instead of 2^63.
+__host__ __device__ __forceinline__ uint64_t from_torus_bits(double x) {
+    const uint64_t b = f64_bits(x);
+    const uint32_t hi = (uint32_t)(b >> 32);
+    const int s = (int)((hi >> 20) & 0x7ff) - 1011;
+    const uint64_t m = (b & 0xFFFFFFFFFFFFFull) | (1ull << 52);
+    uint64_t mag;
+    if (__builtin_expect(s >= 0, 1)) {
+        mag = s < 64 ? m << s : 0;
+    } else {
+        const int k = -s;
+        mag = k < 64 ? (m + (1ull << (k - 1))) >> k : 0;
+    }
+    const uint64_t sg = (uint64_t)(int64_t)((int32_t)hi >> 31);
+    const uint64_t r = (mag ^ sg) - sg;
+    return r - (uint64_t)((sg != 0) & (r == 0x8000000000000000ull));
+}
+
+// tfhe-rs SignedDecomposer (closest_representable + balanced digits, the carry rule of
+// decompose_one_level) for LEV levels of B bits with B * (LEV - 1) < 32: d[l] = the 16-bit two's
+// complement pattern of the digit of level l + 1 (1 = most significant), upper half zero.
+// x + 2^(nrb-1) >> nrb is closest_representable >> nrb (mod 2^(B LEV)), which is all the digits see.
+template <int LEV>
+__host__ __device__ __forceinline__ void decompose16(uint64_t x, int B, uint32_t *d) {
+    const int nrb = 64 - B * LEV;
+    const uint64_t X = x + (1ull << (nrb - 1));
+    const uint32_t mask = (1u << B) - 1, neg = 0x10000u - (1u << B);
+    uint32_t res = (uint32_t)(X >> nrb) & mask;
+    uint32_t st = nrb + B >= 64 ? 0u : (uint32_t)(X >> (nrb + B));
+#pragma unroll
+    for (int l = LEV - 1; l >= 0; l--) {
+        const uint32_t c = (((res - 1) | st) & res) >> (B - 1);
+        d[l] = res + c * neg;  // c in {0, 1}: one v_mad_u32_u24
+        if (l > 0) {
+            st += c;
+            res = st & mask;
+            st >>= B;
+        }
+    }
+}
+
 // pbs_modulus_switch: round(x * 2N / 2^64) in [0, 2N]
 __device__ __forceinline__ int mod_switch(uint64_t x, int logN) {
     uint64_t o = x >> (64 - logN - 2);

@@ -493,9 +493,9 @@ void Engine::init_common() {
     const char *b256 = getenv("TAE_BR_256");
     wide512_ = batched512_ && !(b256 && b256[0] == '1');
     if (batched512_) {
-        HIPC(hipFuncSetAttribute((const void *)br512x2::br_kernel<3, true>,
+        HIPC(hipFuncSetAttribute((const void *)br512x2::br_kernel<3, true, 12>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        HIPC(hipFuncSetAttribute((const void *)br512x2::br_kernel<1, false>,
+        HIPC(hipFuncSetAttribute((const void *)br512x2::br_kernel<1, false, 13>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         HIPC(hipFuncSetAttribute((const void *)br512::br_kernel<kBrC, 3, true>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -642,7 +642,7 @@ void Engine::bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint
         const br512::W16 W = make_w16(w16_);
         const size_t wgs = (B + kBrC - 1) / kBrC;
         if (wide512_) {
-            br512x2::br_kernel<3, true><<<(unsigned)wgs, br512x2::THREADS, br512x2::lds_bytes(), stream_>>>(
+            br512x2::br_kernel<3, true, 12><<<(unsigned)wgs, br512x2::THREADS, br512x2::lds_bytes(), stream_>>>(
                 d_small, p_.n, d_lut_glwe, 0, d_bsk_f_, 0, d_big, (long)B, p_.pbs_b, body_add, out_add, d_twist_, d_w_, W);
             HIPC(hipGetLastError());
             return;
@@ -724,7 +724,7 @@ void Engine::vertical_packing(const cplx *d_ggsw_f, size_t G, int n_in, const ui
         const br512::W16 W = make_w16(w16_);
         const size_t wgs = G * (size_t)((n_out + kBrC - 1) / kBrC);
         if (wide512_) {
-            br512x2::br_kernel<1, false><<<(unsigned)wgs, br512x2::THREADS, br512x2::lds_bytes(), stream_>>>(
+            br512x2::br_kernel<1, false, 13><<<(unsigned)wgs, br512x2::THREADS, br512x2::lds_bytes(), stream_>>>(
                 nullptr, 0, d_lut, n_out, d_ggsw_f, n_in, d_out, (long)G, p_.cbs_b, 0, 0, d_twist_, d_w_, W);
             HIPC(hipGetLastError());
             return;
