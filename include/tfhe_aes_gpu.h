@@ -39,6 +39,10 @@ extern "C" {
 #define TAE_PARAMS_SQRD_LVL_4 1   /* :77-109 */
 #define TAE_PARAMS_SQRD_LVL_64 2  /* :125-157, default (bin/main.rs:82-83) */
 #define TAE_PARAMS_SQRD_LVL_256 3 /* :173-205 */
+/* the 8-bit model's set: src/tfhe/shortint_woppbs_8bit.rs:39-86 (ShortintWoppbs8BitSboxPbsAesEncrypt,
+ * fhe_impls/shortint_woppbs_8bit.rs:44-64).  Bits are LWEs under the SMALL key ([n+1] u64); a byte
+ * is bootstrapped through one 8-bit integer ciphertext (big key, [K+1], plaintext m * 2^56). */
+#define TAE_PARAMS_WOPPBS_8BIT 4
 
 /* memory kinds for the raw-array entry points */
 #define TAE_MEM_HOST 0
@@ -52,13 +56,16 @@ typedef struct tae_lut tae_lut;               /* tfhe::shortint::wopbs::WopbsLUT
 typedef struct {
     int n, k, N, pbs_l, pbs_b, ks_l, ks_b, cbs_l, cbs_b, pfks_l, pfks_b;
     double lwe_std, glwe_std, pfks_std;
-    uint64_t max_noise_sq;
+    uint64_t max_noise_sq; /* 1-bit model: max noise^2; 8-bit model: shortint MaxNoiseLevel (11) */
+    int model;             /* 1 = shortint_woppbs_1bit, 8 = shortint_woppbs_8bit */
 } tae_params;
 
 const char *tae_last_error(void);
 const char *tae_version(void);
 int tae_device_count(int *count);
 int tae_get_params(int param_set, tae_params *out); /* parameters::params_sqrd_lvl_* */
+/* u64 length of one bit ciphertext: K+1 (1-bit model, big key) or n+1 (8-bit model, small key) */
+int tae_bit_len(int param_set, size_t *len);
 
 /* ---- keys (FheContext::generate_keys_with_params, shortint_woppbs_1bit.rs:245-268) ----------
  * Client key generation on the host from a 32-byte seed (ChaCha20 streams, DESIGN.md keygen
@@ -93,6 +100,11 @@ int tae_trivial(const tae_context *ctx, uint64_t bit, tae_bit **out);         /*
 int tae_encrypt_bits_raw(const tae_client_key *ck, const uint8_t *bits, size_t count,
                          uint64_t start_index, uint64_t *out);
 int tae_decrypt_bits_raw(const tae_client_key *ck, const uint64_t *cts, size_t count, uint8_t *bits);
+/* 8-bit model integers (FullWidthCiphertext, shortint_woppbs_8bit.rs:167-178): shortint
+ * encrypt_without_padding / decrypt_without_padding, message modulus 256 ([count][K+1]) */
+int tae_encrypt_ints_raw(const tae_client_key *ck, const uint8_t *values, size_t count, uint64_t start_index,
+                         uint64_t *out);
+int tae_decrypt_ints_raw(const tae_client_key *ck, const uint64_t *cts, size_t count, uint8_t *values);
 
 /* ---- BitCt (shortint_woppbs_1bit.rs:26-151) ----------------------------------------------- */
 int tae_bit_clone(const tae_bit *bit, tae_bit **out);
@@ -116,6 +128,15 @@ int tae_circuit_bootstrap(const tae_context *ctx, const tae_bit *const *bits, si
 int tae_circuit_bootstrap_raw(const tae_context *ctx, const uint64_t *bits, size_t groups,
                               int n_in, const tae_lut *lut, uint64_t *out, int mem);
 
+/* ---- 8-bit model FheContext (shortint_woppbs_8bit.rs:262-336) ------------------------------
+ * generate_lookup_table: tae_generate_lookup_table(ctx, 8, 8, f[256]) (without-padding LUT);
+ * tae_circuit_bootstrap[_raw] with n_in = 8 runs Byte::bootstrap_with_lut (8 bits -> 8 bits).
+ * bootstrap_from_bits: bits [groups][8][n+1] -> ints [groups][K+1] */
+int tae_bootstrap_from_bits_raw(const tae_context *ctx, const uint64_t *bits, size_t groups, const tae_lut *lut,
+                                uint64_t *out, int mem);
+/* extract_bits_from_ciphertext: ints [groups][K+1] -> bits [groups][8][n+1], MSB first */
+int tae_extract_bits_raw(const tae_context *ctx, const uint64_t *ints, size_t groups, uint64_t *out, int mem);
+
 /* ---- Aes128Encrypt for ShortintWoppbs1BitSboxGalMulPbsAesEncrypt -------------------------
  *      (src/aes_128/fhe.rs:16-38, fhe_impls/shortint_woppbs_1bit.rs:131-151,
  *       fhe_sbox_gal_mul_pbs.rs:84-191) */
@@ -127,10 +148,13 @@ int tae_aes_encrypt_blocks(const tae_context *ctx, const tae_bit *const *expande
                            const tae_bit *const *blocks, size_t n_blocks, int rounds, tae_bit **out);
 /* key_schedule (fhe_sbox_gal_mul_pbs.rs:134-164): key[128] bits -> expanded[44*32] bits */
 int tae_aes_key_schedule(const tae_context *ctx, const tae_bit *const *key, tae_bit **expanded);
-/* raw arrays: rk [44*32][K+1], blocks [n][128][K+1], out [n][128][K+1]; inputs fresh
- * (noise level 1) -- the noise schedule of the round function is validated statically. */
+/* raw arrays: rk [44*32][L], blocks [n][128][L], out [n][128][L] with L = tae_bit_len (K+1, or
+ * n+1 for the 8-bit model's ShortintWoppbs8BitSboxPbsAesEncrypt / fhe_sbox_pbs.rs:75-121); inputs
+ * fresh (noise level 1) -- the noise schedule of the round function is validated statically. */
 int tae_aes_encrypt_blocks_raw(const tae_context *ctx, const uint64_t *rk, const uint64_t *blocks,
                                size_t n_blocks, int rounds, uint64_t *out, int mem);
+/* key_schedule on raw fresh key bits [128][L] -> [44*32][L] (either model) */
+int tae_aes_key_schedule_raw(const tae_context *ctx, const uint64_t *key, uint64_t *expanded, int mem);
 
 /* ---- stage entry points (raw arrays; parity tests and profiling) ---------------------------- */
 int tae_stage_keyswitch(const tae_context *ctx, const uint64_t *in, size_t count, uint64_t *out, int mem);

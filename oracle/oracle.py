@@ -15,6 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _SO = os.path.join(_HERE, "build", "liboracle.so")
 
 PARAMS_SQRD_LVL_1, PARAMS_SQRD_LVL_4, PARAMS_SQRD_LVL_64, PARAMS_SQRD_LVL_256 = 0, 1, 2, 3
+PARAMS_WOPPBS_8BIT = 4  # shortint_woppbs_8bit.rs:39-86
 
 
 def build() -> str:
@@ -104,6 +105,20 @@ def lib():
         L.or_sub_bytes_gal_mul.argtypes = [C.c_void_p, u64p, C.c_int, C.c_int, u64p]
         L.or_plain_key_schedule.argtypes = [C.c_char_p, C.c_char_p]
         L.or_plain_encrypt_block.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_char_p]
+        L.or_cbs_vp_small.argtypes = [C.c_void_p, u64p, C.c_int, u64p, C.c_int, u64p]
+        L.or_encrypt_small_bit.argtypes = [C.c_void_p, C.c_char_p, C.c_uint64, C.c_uint64, u64p]
+        L.or_decrypt_small_bit.argtypes = [C.c_void_p, u64p]
+        L.or_decrypt_small_bit.restype = C.c_uint64
+        L.or_encrypt_int.argtypes = [C.c_void_p, C.c_char_p, C.c_uint64, C.c_uint64, u64p]
+        L.or_decrypt_int.argtypes = [C.c_void_p, u64p]
+        L.or_decrypt_int.restype = C.c_uint64
+        L.or_generate_lut_without_padding.argtypes = [C.c_int, u64p, u64p]
+        L.or_extract_bits.argtypes = [C.c_void_p, u64p, C.c_int, C.c_int, u64p]
+        L.or_bootstrap_with_lut8.argtypes = [C.c_void_p, u64p, u64p, u64p]
+        L.or_gf_256_mul_terms.argtypes = [C.c_uint8, C.c_void_p]
+        L.or_mix_column_terms.argtypes = [C.c_void_p]
+        L.or_sub_bytes8.argtypes = [C.c_void_p, u64p, C.c_int, C.c_int, u64p]
+        L.or_aes8_encrypt_block.argtypes = [C.c_void_p, u64p, u64p, C.c_int, C.c_int, u64p]
         L.or_gf_256_mul_quirk.argtypes = [C.c_uint8, C.c_uint8]
         L.or_gf_256_mul_quirk.restype = C.c_uint8
         _lib = L
@@ -252,6 +267,78 @@ class Keys:
         lib().or_aes_encrypt_block(self.sk, _p64(np.ascontiguousarray(rk)), _p64(np.ascontiguousarray(block)),
                                    rounds, threads, _p64(out))
         return out
+
+    # --- 8-bit model (param id 4) ---
+    def encrypt_small_bits(self, bits, seed: bytes, start_index: int = 0) -> np.ndarray:
+        out = np.zeros((len(bits), self.p["n"] + 1), dtype=np.uint64)
+        for i, b in enumerate(bits):
+            lib().or_encrypt_small_bit(self.ck, seed, start_index + i, int(b), _p64(out[i]))
+        return out
+
+    def decrypt_small_bits(self, cts: np.ndarray) -> np.ndarray:
+        cts = np.ascontiguousarray(cts.reshape(-1, self.p["n"] + 1))
+        return np.array([lib().or_decrypt_small_bit(self.ck, _p64(cts[i])) for i in range(cts.shape[0])],
+                        dtype=np.uint8)
+
+    def encrypt_ints(self, values, seed: bytes, start_index: int = 0) -> np.ndarray:
+        out = np.zeros((len(values), self.K + 1), dtype=np.uint64)
+        for i, v in enumerate(values):
+            lib().or_encrypt_int(self.ck, seed, start_index + i, int(v), _p64(out[i]))
+        return out
+
+    def decrypt_ints(self, cts: np.ndarray) -> np.ndarray:
+        cts = np.ascontiguousarray(cts.reshape(-1, self.K + 1))
+        return np.array([lib().or_decrypt_int(self.ck, _p64(cts[i])) for i in range(cts.shape[0])], dtype=np.uint64)
+
+    def cbs_vp_small(self, bits: np.ndarray, lut: np.ndarray, n_out: int) -> np.ndarray:
+        bits = np.ascontiguousarray(bits, dtype=np.uint64)
+        out = np.zeros((n_out, self.K + 1), dtype=np.uint64)
+        lib().or_cbs_vp_small(self.sk, _p64(bits), bits.shape[0], _p64(np.ascontiguousarray(lut, dtype=np.uint64)),
+                              n_out, _p64(out))
+        return out
+
+    def extract_bits(self, ct: np.ndarray, delta_log: int = 56, nbits: int = 8) -> np.ndarray:
+        out = np.zeros((nbits, self.p["n"] + 1), dtype=np.uint64)
+        lib().or_extract_bits(self.sk, _p64(np.ascontiguousarray(ct, dtype=np.uint64)), delta_log, nbits, _p64(out))
+        return out
+
+    def bootstrap_with_lut8(self, bits: np.ndarray, lut: np.ndarray) -> np.ndarray:
+        out = np.zeros((8, self.p["n"] + 1), dtype=np.uint64)
+        lib().or_bootstrap_with_lut8(self.sk, _p64(np.ascontiguousarray(bits, dtype=np.uint64)),
+                                     _p64(np.ascontiguousarray(lut, dtype=np.uint64)), _p64(out))
+        return out
+
+    def sub_bytes8(self, state: np.ndarray, threads: int = 8) -> np.ndarray:
+        state = np.ascontiguousarray(state, dtype=np.uint64)
+        nb = state.size // (8 * (self.p["n"] + 1))
+        out = np.zeros((nb, 8, self.p["n"] + 1), dtype=np.uint64)
+        lib().or_sub_bytes8(self.sk, _p64(state), nb, threads, _p64(out))
+        return out
+
+    def aes8_encrypt_block(self, rk: np.ndarray, block: np.ndarray, rounds: int, threads: int = 8):
+        out = np.zeros((128, self.p["n"] + 1), dtype=np.uint64)
+        lib().or_aes8_encrypt_block(self.sk, _p64(np.ascontiguousarray(rk, dtype=np.uint64)),
+                                    _p64(np.ascontiguousarray(block, dtype=np.uint64)), rounds, threads, _p64(out))
+        return out
+
+
+def generate_lut_without_padding(N: int, f) -> np.ndarray:
+    tab = np.array([f(v) for v in range(256)], dtype=np.uint64)
+    out = np.zeros(max(N, 256), dtype=np.uint64)
+    lib().or_generate_lut_without_padding(N, _p64(tab), _p64(out))
+    return out
+
+
+def gf_256_mul_terms(b: int) -> np.ndarray:
+    out = np.zeros((8, 8), dtype=np.int32)
+    lib().or_gf_256_mul_terms(b, out.ctypes.data_as(C.c_void_p))
+    return out
+
+
+def mix_column_terms() -> np.ndarray:
+    out = np.zeros((32, 32), dtype=np.int32)
+    lib().or_mix_column_terms(out.ctypes.data_as(C.c_void_p))
+    return out
 
 
 def generate_lut(N: int, input_bits: int, output_bits: int, f) -> np.ndarray:

@@ -39,6 +39,12 @@ int or_params_get(int id, or_params *o) {
         *o = (or_params){665, 2, 1024, 4, 9, 6, 2, 1, 14, 3, 12,
                          4.7280002450549286e-05, 3.162026630747649e-16, 3.162026630747649e-16, 256};
         return 0;
+    case 4: /* shortint_woppbs_8bit params(), shortint_woppbs_8bit.rs:39-86; max_noise_sq holds the
+             * shortint MaxNoiseLevel (11, additive levels), not a squared level */
+        *o = (or_params){785, 2, 1024, 6, 7, 8, 2, 4, 6, 3, 12,
+                         1.5140301927925663e-05, 0.00000000000000022148688116005568,
+                         0.00000000000000022148688116005568, 11};
+        return 0;
     default:
         return -1;
     }
@@ -126,7 +132,7 @@ static uint64_t rng_gauss_torus(rng_t *r, double sigma) {
 }
 
 /* keygen stream purposes (spec shared with the product client) */
-enum { P_LWE_SK = 1, P_GLWE_SK = 2, P_KSK = 3, P_BSK = 4, P_PFPKSK = 5, P_ENCRYPT = 6 };
+enum { P_LWE_SK = 1, P_GLWE_SK = 2, P_KSK = 3, P_BSK = 4, P_PFPKSK = 5, P_ENCRYPT = 6, P_ENCRYPT_INT = 7 };
 #define CT_STRIDE (1ull << 24)
 
 /* ======================================================================================
@@ -897,19 +903,35 @@ void or_circuit_bootstrap(const or_server_key *sk, const uint64_t *bits, int n_i
     size_t glwe = (size_t)(k + 1) * N;
     size_t ggsw_std = (size_t)p->cbs_l * (k + 1) * glwe;
     size_t ggsw_f = (size_t)p->cbs_l * (k + 1) * (k + 1) * M;
-    uint64_t *small = (uint64_t *)malloc(sizeof(uint64_t) * (n + 1));
+    (void)M;
+    (void)ggsw_std;
+    (void)ggsw_f;
+    uint64_t *small = (uint64_t *)malloc(sizeof(uint64_t) * (n + 1) * n_in);
+    for (int b = 0; b < n_in; b++) or_keyswitch(sk, bits + (size_t)b * (K + 1), small + (size_t)b * (n + 1));
+    or_cbs_vp_small(sk, small, n_in, lut, n_out, out);
+    free(small);
+}
+
+/* circuit_bootstrap_boolean_vertical_packing on small-key bits (tfhe-rs wop_pbs; the 8-bit model's
+ * WopbsKey::circuit_bootstrapping_vertical_packing, shortint_woppbs_8bit.rs:299-335): bits
+ * [n_in][n+1] (MSB first), lut [n_out][small_len], out [n_out][K+1] */
+void or_cbs_vp_small(const or_server_key *sk, const uint64_t *bits, int n_in, const uint64_t *lut, int n_out,
+                     uint64_t *out) {
+    const or_params *p = &sk->p;
+    int n = p->n, k = p->k, N = p->N, M = N / 2, K = k * N;
+    size_t glwe = (size_t)(k + 1) * N;
+    size_t ggsw_std = (size_t)p->cbs_l * (k + 1) * glwe;
+    size_t ggsw_f = (size_t)p->cbs_l * (k + 1) * (k + 1) * M;
     uint64_t *g = (uint64_t *)malloc(sizeof(uint64_t) * ggsw_std);
     or_c64 *gf = (or_c64 *)malloc(sizeof(or_c64) * ggsw_f * n_in);
     for (int b = 0; b < n_in; b++) {
-        or_keyswitch(sk, bits + (size_t)b * (K + 1), small);
-        or_circuit_bootstrap_boolean(sk, small, g);
+        or_circuit_bootstrap_boolean(sk, bits + (size_t)b * (n + 1), g);
         or_ggsw_to_fourier(sk, g, p->cbs_l, gf + (size_t)b * ggsw_f);
     }
     size_t small_len = or_lut_small_len(N, n_in);
     int n_polys = (int)(small_len / N);
     for (int j = 0; j < n_out; j++)
         or_vertical_packing(sk, lut + (size_t)j * small_len, n_polys, gf, n_in, out + (size_t)j * (K + 1));
-    free(small);
     free(g);
     free(gf);
 }
@@ -1095,4 +1117,197 @@ void or_aes_encrypt_block(const or_server_key *sk, const uint64_t *rk, const uin
     free(muls);
     free(lut24);
     free(lut8);
+}
+
+/* ======================================================================================
+ * 8-bit model (src/tfhe/shortint_woppbs_8bit.rs, src/aes_128/fhe/fhe_impls/shortint_woppbs_8bit.rs,
+ * src/aes_128/fhe/fhe_sbox_pbs.rs)
+ * ====================================================================================== */
+/* ClientKey::encrypt (shortint_woppbs_8bit.rs:199-214): LWE under the SMALL key, lwe noise */
+void or_encrypt_small_bit(const or_client_key *ck, const uint8_t seed[32], uint64_t index, uint64_t bit,
+                          uint64_t *out) {
+    lwe_encrypt(ck->lwe_sk, ck->p.n, or_encode_bit(bit), ck->p.lwe_std, seed, P_ENCRYPT, index, out);
+}
+uint64_t or_decrypt_small_bit(const or_client_key *ck, const uint64_t *ct) {
+    return or_decode_bit(or_decrypt_small_phase(ck, ct));
+}
+/* shortint ClientKey::encrypt_without_padding (EncryptionKeyChoice::Big: big key, glwe noise),
+ * message modulus 256, carry 1: plaintext = m * 2^56 (test inputs for extract_bits) */
+void or_encrypt_int(const or_client_key *ck, const uint8_t seed[32], uint64_t index, uint64_t value,
+                    uint64_t *out) {
+    lwe_encrypt(ck->glwe_sk, ck->p.k * ck->p.N, (value & 255) << 56, ck->p.glwe_std, seed, P_ENCRYPT_INT, index,
+                out);
+}
+/* decrypt_without_padding: round(phase / 2^56) mod 256 */
+uint64_t or_decrypt_int(const or_client_key *ck, const uint64_t *ct) {
+    uint64_t ph = or_decrypt_phase(ck, ct);
+    return ((ph + (1ull << 55)) >> 56) & 255;
+}
+
+/* WopbsKey::generate_lut_without_padding (tfhe-rs shortint/wopbs, called by
+ * FheContext::generate_lookup_table, shortint_woppbs_8bit.rs:262-265) for message modulus 256,
+ * carry 1: lut[i] = (f(i mod 256) mod 256) << 56 over max(256, N) entries */
+void or_generate_lut_without_padding(int N, const uint64_t *f_table, uint64_t *out) {
+    int size = N > 256 ? N : 256;
+    for (int i = 0; i < size; i++) out[i] = (f_table[i & 255] & 255) << 56;
+}
+
+/* tfhe-rs fft64::crypto::wop_pbs::extract_bits (shortint_woppbs_8bit.rs:268-296 calls it through
+ * WopbsKey::extract_bits with DeltaLog(56), ExtractedBitsCount(8)): big-key lwe_in [K+1] ->
+ * out [nbits][n+1] small-key bit ciphertexts, MSB first.  Bit bit_idx (LSB first): shift it to the
+ * MSB, keyswitch (the output), then unless it is the last: PBS of (ks + q/4) with the accumulator
+ * -alpha, alpha = 2^(delta_log - 1 + bit_idx), + alpha, and subtract from the input. */
+void or_extract_bits(const or_server_key *sk, const uint64_t *lwe_in, int delta_log, int nbits, uint64_t *out) {
+    const or_params *p = &sk->p;
+    int n = p->n, k = p->k, N = p->N, K = k * N;
+    size_t glwe = (size_t)(k + 1) * N;
+    uint64_t *buf = (uint64_t *)malloc(sizeof(uint64_t) * (K + 1));
+    uint64_t *sh = (uint64_t *)malloc(sizeof(uint64_t) * (K + 1));
+    uint64_t *pbs = (uint64_t *)malloc(sizeof(uint64_t) * (K + 1));
+    uint64_t *ks = (uint64_t *)malloc(sizeof(uint64_t) * (n + 1));
+    uint64_t *acc = (uint64_t *)calloc(glwe, sizeof(uint64_t));
+    memcpy(buf, lwe_in, sizeof(uint64_t) * (K + 1));
+    for (int bit_idx = 0; bit_idx < nbits; bit_idx++) {
+        int shift = 64 - delta_log - bit_idx - 1;
+        for (int i = 0; i <= K; i++) sh[i] = buf[i] << shift;
+        or_keyswitch(sk, sh, ks);
+        memcpy(out + (size_t)(nbits - 1 - bit_idx) * (n + 1), ks, sizeof(uint64_t) * (n + 1));
+        if (bit_idx == nbits - 1) break;
+        ks[n] += 1ull << 62;
+        uint64_t alpha = 1ull << (delta_log - 1 + bit_idx);
+        for (int j = 0; j < N; j++) acc[(size_t)k * N + j] = 0 - alpha;
+        or_bootstrap(sk, ks, acc, pbs);
+        pbs[K] += alpha;
+        for (int i = 0; i <= K; i++) buf[i] -= pbs[i];
+    }
+    free(buf);
+    free(sh);
+    free(pbs);
+    free(ks);
+    free(acc);
+}
+
+/* Byte::bootstrap_with_lut (fhe_impls/shortint_woppbs_8bit.rs:37-42): bootstrap_from_bits
+ * (CBS-VP of the 8 small-key bits with a without-padding LUT -> one big-key int ciphertext), then
+ * extract_bits_from_ciphertext.  bits/out [8][n+1], lut [N] */
+void or_bootstrap_with_lut8(const or_server_key *sk, const uint64_t *bits, const uint64_t *lut, uint64_t *out) {
+    int K = sk->p.k * sk->p.N;
+    uint64_t *ict = (uint64_t *)malloc(sizeof(uint64_t) * (K + 1));
+    or_cbs_vp_small(sk, bits, 8, lut, 1, ict);
+    or_extract_bits(sk, ict, 56, 8, out);
+    free(ict);
+}
+
+/* fhe_sbox_pbs::gf_256_mul (:33-53) on symbolic bytes: coef[o][i] = how many times input bit i
+ * (MSB-first) is added into output bit o (XORs are LWE additions, so nothing cancels) */
+void or_gf_256_mul_terms(uint8_t b, int coef[8][8]) {
+    int a[8][8], res[8][8];
+    memset(a, 0, sizeof(a));
+    memset(res, 0, sizeof(res));
+    for (int i = 0; i < 8; i++) a[i][i] = 1;
+    for (int it = 0; it < 8; it++) {
+        if (b & 1)
+            for (int o = 0; o < 8; o++)
+                for (int i = 0; i < 8; i++) res[o][i] += a[o][i];
+        int red[8];
+        memcpy(red, a[0], sizeof(red)); /* shl_assign_1: old a[0] out, rotate left, trivial 0 in */
+        for (int o = 0; o < 7; o++) memcpy(a[o], a[o + 1], sizeof(red));
+        memset(a[7], 0, sizeof(red));
+        const int taps[4] = {3, 4, 6, 7};
+        for (int t = 0; t < 4; t++)
+            for (int i = 0; i < 8; i++) a[taps[t]][i] += red[i];
+        b >>= 1;
+    }
+    memcpy(coef, res, sizeof(res));
+}
+
+/* MixColumns of fhe_sbox_pbs (:56-73) as a linear map on one column's 32 bits:
+ * coef[32 out][32 in], byte-major, MSB-first bits */
+void or_mix_column_terms(int coef[32][32]) {
+    int g1[8][8], g2[8][8], g3[8][8];
+    or_gf_256_mul_terms(1, g1);
+    or_gf_256_mul_terms(2, g2);
+    or_gf_256_mul_terms(3, g3);
+    memset(coef, 0, sizeof(int) * 32 * 32);
+    for (int i = 0; i < 4; i++)
+        for (int o = 0; o < 8; o++)
+            for (int x = 0; x < 8; x++) {
+                coef[8 * i + o][8 * i + x] += g2[o][x];
+                coef[8 * i + o][8 * ((i + 3) % 4) + x] += g1[o][x];
+                coef[8 * i + o][8 * ((i + 2) % 4) + x] += g1[o][x];
+                coef[8 * i + o][8 * ((i + 1) % 4) + x] += g3[o][x];
+            }
+}
+
+typedef struct {
+    const or_server_key *sk;
+    const uint64_t *in, *lut;
+    uint64_t *out;
+    int n_bytes, tid, nthreads;
+} sb8_job;
+
+static void *sb8_worker(void *arg) {
+    sb8_job *J = (sb8_job *)arg;
+    size_t byte_sz = (size_t)8 * (J->sk->p.n + 1);
+    for (int b = J->tid; b < J->n_bytes; b += J->nthreads)
+        or_bootstrap_with_lut8(J->sk, J->in + b * byte_sz, J->lut, J->out + b * byte_sz);
+    return NULL;
+}
+
+/* SubBytes of fhe_sbox_pbs (:23-31) with ByteT::sbox_substitute of the 8-bit model, threads over bytes */
+void or_sub_bytes8(const or_server_key *sk, const uint64_t *state, int n_bytes, int threads, uint64_t *out) {
+    int N = sk->p.N;
+    uint64_t f[256];
+    for (int x = 0; x < 256; x++) f[x] = or_sbox[x];
+    uint64_t *lut = (uint64_t *)malloc(sizeof(uint64_t) * (N > 256 ? N : 256));
+    or_generate_lut_without_padding(N, f, lut);
+    if (threads < 1) threads = 1;
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * threads);
+    sb8_job *jobs = (sb8_job *)malloc(sizeof(sb8_job) * threads);
+    for (int t = 0; t < threads; t++) {
+        jobs[t] = (sb8_job){sk, state, lut, out, n_bytes, t, threads};
+        pthread_create(&th[t], NULL, sb8_worker, &jobs[t]);
+    }
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    free(th);
+    free(jobs);
+    free(lut);
+}
+
+/* fhe_sbox_pbs::encrypt_block_for_rounds (:75-121) on small-key bit arrays: rk [44*32][n+1],
+ * block/out [128][n+1] (block byte order, MSB-first bits) */
+void or_aes8_encrypt_block(const or_server_key *sk, const uint64_t *rk, const uint64_t *block, int rounds,
+                           int threads, uint64_t *out) {
+    int L = sk->p.n + 1;
+    size_t byte_sz = (size_t)8 * L;
+    uint64_t *state = (uint64_t *)malloc(sizeof(uint64_t) * 16 * byte_sz);
+    uint64_t *sb = (uint64_t *)malloc(sizeof(uint64_t) * 16 * byte_sz);
+    int coef[32][32];
+    or_mix_column_terms(coef);
+    memcpy(state, block, sizeof(uint64_t) * 16 * byte_sz);
+    for (int i = 0; i < 128; i++) lwe_add(state + (size_t)i * L, rk + (size_t)i * L, L);
+    for (int r = 1; r <= rounds; r++) {
+        int last = r == rounds;
+        or_sub_bytes8(sk, state, 16, threads, sb);
+        /* shift_rows: state[row][c] = sb[row][(c + row) % 4]; byte index 4c + row */
+        for (int c = 0; c < 4; c++)
+            for (int row = 0; row < 4; row++)
+                memcpy(state + (size_t)(4 * c + row) * byte_sz, sb + (size_t)(4 * ((c + row) % 4) + row) * byte_sz,
+                       sizeof(uint64_t) * byte_sz);
+        if (!last) {
+            memcpy(sb, state, sizeof(uint64_t) * 16 * byte_sz);
+            for (int c = 0; c < 4; c++)
+                for (int o = 0; o < 32; o++) {
+                    uint64_t *dst = state + ((size_t)32 * c + o) * L;
+                    memset(dst, 0, sizeof(uint64_t) * L);
+                    for (int i = 0; i < 32; i++)
+                        for (int t = 0; t < coef[o][i]; t++) lwe_add(dst, sb + ((size_t)32 * c + i) * L, L);
+                }
+        }
+        const uint64_t *k = rk + (size_t)(last ? 160 : 16 * r) * byte_sz;
+        for (int i = 0; i < 128; i++) lwe_add(state + (size_t)i * L, k + (size_t)i * L, L);
+    }
+    memcpy(out, state, sizeof(uint64_t) * 16 * byte_sz);
+    free(state);
+    free(sb);
 }

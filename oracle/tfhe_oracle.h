@@ -54,7 +54,8 @@ typedef struct {
     uint64_t max_noise_sq;
 } or_params;
 
-/* 0 = params_sqrd_lvl_1 (:29), 1 = _4 (:77), 2 = _64 (:125), 3 = _256 (:173) */
+/* 0 = params_sqrd_lvl_1 (:29), 1 = _4 (:77), 2 = _64 (:125), 3 = _256 (:173),
+ * 4 = shortint_woppbs_8bit params() (shortint_woppbs_8bit.rs:39-86) */
 int or_params_get(int id, or_params *out);
 
 /* ---------------- randomness (keygen spec shared with the product) ---------- */
@@ -147,6 +148,26 @@ void or_vertical_packing(const or_server_key *sk, const uint64_t *lut, int n_pol
 /* FheContext::circuit_bootstrap: bits [n_in][K+1], lut [n_out][small_len], out [n_out][K+1] */
 void or_circuit_bootstrap(const or_server_key *sk, const uint64_t *bits, int n_in,
                           const uint64_t *lut, int n_out, uint64_t *out);
+
+/* circuit_bootstrap_boolean_vertical_packing on small-key bits [n_in][n+1] (no keyswitch) */
+void or_cbs_vp_small(const or_server_key *sk, const uint64_t *bits, int n_in, const uint64_t *lut, int n_out,
+                     uint64_t *out);
+
+/* ---------------- 8-bit model (param id 4: shortint_woppbs_8bit.rs:39-86) ---------------- */
+void or_encrypt_small_bit(const or_client_key *ck, const uint8_t seed[32], uint64_t index, uint64_t bit,
+                          uint64_t *out /*[n+1]*/);
+uint64_t or_decrypt_small_bit(const or_client_key *ck, const uint64_t *ct);
+void or_encrypt_int(const or_client_key *ck, const uint8_t seed[32], uint64_t index, uint64_t value,
+                    uint64_t *out /*[K+1]*/);
+uint64_t or_decrypt_int(const or_client_key *ck, const uint64_t *ct);
+void or_generate_lut_without_padding(int N, const uint64_t *f_table /*[256]*/, uint64_t *out /*[max(N,256)]*/);
+void or_extract_bits(const or_server_key *sk, const uint64_t *lwe_in, int delta_log, int nbits, uint64_t *out);
+void or_bootstrap_with_lut8(const or_server_key *sk, const uint64_t *bits, const uint64_t *lut, uint64_t *out);
+void or_gf_256_mul_terms(uint8_t b, int coef[8][8]);
+void or_mix_column_terms(int coef[32][32]);
+void or_sub_bytes8(const or_server_key *sk, const uint64_t *state, int n_bytes, int threads, uint64_t *out);
+void or_aes8_encrypt_block(const or_server_key *sk, const uint64_t *rk, const uint64_t *block, int rounds,
+                           int threads, uint64_t *out);
 
 /* generate_multivariate_luts: f_table[1<<input_bits]; out [output_bits][N << tree_bits] */
 size_t or_lut_small_len(int N, int input_bits);

@@ -57,3 +57,24 @@ def golden():
     import json
     with open(os.path.join(ROOT, "tests", "golden", "aes_golden.json")) as fh:
         return json.load(fh)
+
+
+# ---- 8-bit model (param set 4, shortint_woppbs_8bit.rs:39-86) ----
+@pytest.fixture(scope="session")
+def oracle_keys8(oracle_mod):
+    return oracle_mod.Keys(oracle_mod.PARAMS_WOPPBS_8BIT, SEED, threads=min(16, os.cpu_count() or 1))
+
+
+@pytest.fixture(scope="session")
+def product_raw8():
+    import tfhe_aes
+    return tfhe_aes.generate_keys_raw(tfhe_aes.PARAMS_WOPPBS_8BIT, SEED, threads=min(16, os.cpu_count() or 1))
+
+
+@pytest.fixture(scope="session")
+def gpu_context8(product_raw8):
+    import tfhe_aes
+    if tfhe_aes.device_count() < 1:
+        pytest.fail("no GPU visible: -m gpu tests must run on the MI355X box")
+    _, keys = product_raw8
+    return tfhe_aes.context_from_raw(tfhe_aes.PARAMS_WOPPBS_8BIT, keys, device=0)

@@ -9,8 +9,10 @@ from tfhe_aes import Cleartext, aes_128
 
 def test_params_match_reference(oracle_mod):
     # parameters.rs:29-205
-    for pid in range(4):
-        assert tfhe_aes.get_params(pid) == oracle_mod.params(pid)
+    for pid in range(5):
+        prod = tfhe_aes.get_params(pid)
+        assert prod.pop("model") == (8 if pid == tfhe_aes.PARAMS_WOPPBS_8BIT else 1)
+        assert prod == oracle_mod.params(pid)
     p = tfhe_aes.get_params(tfhe_aes.PARAMS_SQRD_LVL_64)
     assert (p["n"], p["k"], p["N"], p["pbs_l"], p["pbs_b"], p["ks_l"], p["ks_b"], p["cbs_l"], p["cbs_b"],
             p["pfks_l"], p["pfks_b"], p["max_noise_sq"]) == (677, 4, 512, 3, 12, 4, 3, 1, 13, 2, 16, 64)

@@ -64,7 +64,7 @@ tae::Params params_of(int param_set) {
 
 void fill(tae_params *o, const tae::Params &p) {
     *o = {p.n, p.k, p.N, p.pbs_l, p.pbs_b, p.ks_l, p.ks_b, p.cbs_l, p.cbs_b, p.pfks_l, p.pfks_b,
-          p.lwe_std, p.glwe_std, p.pfks_std, p.max_noise_sq};
+          p.lwe_std, p.glwe_std, p.pfks_std, p.max_noise_sq, p.model};
 }
 
 void require_device(int device) {
@@ -139,6 +139,14 @@ int tae_get_params(int param_set, tae_params *out) {
     return guarded([&] {
         require(out, "null");
         fill(out, params_of(param_set));
+    });
+}
+
+int tae_bit_len(int param_set, size_t *len) {
+    return guarded([&] {
+        require(len, "null");
+        const tae::Params p = params_of(param_set);
+        *len = p.model == 8 ? p.small_len() : p.big_len();
     });
 }
 
@@ -236,9 +244,10 @@ int tae_encrypt(const tae_client_key *ck, uint64_t bit, tae_bit **out) {
         if (bit > 1) throw tae::ModelError{TAE_E_ARG, "cleartext out of bounds: " + std::to_string(bit)};
         auto &c = const_cast<tae_client_key *>(ck)->ck;
         auto b = std::make_unique<tae_bit>();
-        b->b.ct.assign(c.p.big_len(), 0);
-        c.encrypt_bit_at(bit, c.next_index.fetch_add(1), b->b.ct.data());
-        b->b.noise = tae::NoiseLevel::with_noise_level(1, tae::next_ct_id());  // BitCt::fresh
+        b->b.ct.assign(c.bit_len(), 0);
+        c.encrypt_model_bit_at(bit, c.next_index.fetch_add(1), b->b.ct.data());
+        // BitCt::fresh (1-bit model: noise^2 1 + a new component id; 8-bit: NoiseLevel::NOMINAL)
+        b->b.noise = c.p.model == 8 ? tae::NoiseLevel{1, {}} : tae::NoiseLevel::with_noise_level(1, tae::next_ct_id());
         b->b.max_noise_sq = c.p.max_noise_sq;
         *out = b.release();
     });
@@ -247,8 +256,8 @@ int tae_encrypt(const tae_client_key *ck, uint64_t bit, tae_bit **out) {
 int tae_decrypt(const tae_client_key *ck, const tae_bit *bit, uint64_t *out) {
     return guarded([&] {
         require(ck && bit && out, "null");
-        require(bit->b.ct.size() == ck->ck.p.big_len(), "ciphertext size mismatch");
-        *out = ck->ck.decrypt_bit(bit->b.ct.data());
+        require(bit->b.ct.size() == ck->ck.bit_len(), "ciphertext size mismatch");
+        *out = ck->ck.decrypt_model_bit(bit->b.ct.data());
     });
 }
 
@@ -263,19 +272,36 @@ int tae_encrypt_bits_raw(const tae_client_key *ck, const uint8_t *bits, size_t c
                          uint64_t *out) {
     return guarded([&] {
         require(ck && (bits || !count) && (out || !count), "null");
-        const size_t L = ck->ck.p.big_len();
+        const size_t L = ck->ck.bit_len();
         for (size_t i = 0; i < count; i++) {
             require(bits[i] < 2, "cleartext out of bounds");
-            ck->ck.encrypt_bit_at(bits[i], start_index + i, out + i * L);
+            ck->ck.encrypt_model_bit_at(bits[i], start_index + i, out + i * L);
         }
+    });
+}
+
+int tae_encrypt_ints_raw(const tae_client_key *ck, const uint8_t *values, size_t count, uint64_t start_index,
+                         uint64_t *out) {
+    return guarded([&] {
+        require(ck && (values || !count) && (out || !count), "null");
+        const size_t L = ck->ck.p.big_len();
+        for (size_t i = 0; i < count; i++) ck->ck.encrypt_int_at(values[i], start_index + i, out + i * L);
+    });
+}
+
+int tae_decrypt_ints_raw(const tae_client_key *ck, const uint64_t *cts, size_t count, uint8_t *values) {
+    return guarded([&] {
+        require(ck && (cts || !count) && (values || !count), "null");
+        const size_t L = ck->ck.p.big_len();
+        for (size_t i = 0; i < count; i++) values[i] = (uint8_t)ck->ck.decrypt_int(cts + i * L);
     });
 }
 
 int tae_decrypt_bits_raw(const tae_client_key *ck, const uint64_t *cts, size_t count, uint8_t *bits) {
     return guarded([&] {
         require(ck && (cts || !count) && (bits || !count), "null");
-        const size_t L = ck->ck.p.big_len();
-        for (size_t i = 0; i < count; i++) bits[i] = (uint8_t)ck->ck.decrypt_bit(cts + i * L);
+        const size_t L = ck->ck.bit_len();
+        for (size_t i = 0; i < count; i++) bits[i] = (uint8_t)ck->ck.decrypt_model_bit(cts + i * L);
     });
 }
 
@@ -313,7 +339,7 @@ int tae_bit_data(const tae_bit *bit, uint64_t *out, size_t len) {
 int tae_bit_from_data(const tae_context *ctx, const uint64_t *data, size_t len, uint64_t nl, tae_bit **out) {
     return guarded([&] {
         require(ctx && data && out, "null");
-        require(len == ctx->ctx->params().big_len(), "length mismatch");
+        require(len == ctx->ctx->bit_len(), "length mismatch");
         *out = new tae_bit{ctx->ctx->wrap(std::vector<uint64_t>(data, data + len), nl)};
     });
 }
@@ -352,6 +378,28 @@ int tae_circuit_bootstrap_raw(const tae_context *ctx, const uint64_t *bits, size
     return guarded([&] {
         require(ctx && bits && lut && out, "null");
         ctx->ctx->circuit_bootstrap_raw(bits, groups, n_in, lut->l, out, mem == TAE_MEM_DEVICE);
+    });
+}
+
+int tae_bootstrap_from_bits_raw(const tae_context *ctx, const uint64_t *bits, size_t groups, const tae_lut *lut,
+                                uint64_t *out, int mem) {
+    return guarded([&] {
+        require(ctx && bits && lut && out, "null");
+        ctx->ctx->bootstrap_from_bits_raw(bits, groups, lut->l, out, mem == TAE_MEM_DEVICE);
+    });
+}
+
+int tae_extract_bits_raw(const tae_context *ctx, const uint64_t *ints, size_t groups, uint64_t *out, int mem) {
+    return guarded([&] {
+        require(ctx && ints && out, "null");
+        ctx->ctx->extract_bits_raw(ints, groups, out, mem == TAE_MEM_DEVICE);
+    });
+}
+
+int tae_aes_key_schedule_raw(const tae_context *ctx, const uint64_t *key, uint64_t *expanded, int mem) {
+    return guarded([&] {
+        require(ctx && key && expanded, "null");
+        ctx->ctx->aes_key_schedule_raw(key, expanded, mem == TAE_MEM_DEVICE);
     });
 }
 

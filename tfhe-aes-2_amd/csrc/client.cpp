@@ -2,6 +2,8 @@
 // See client.hpp for the reference mapping.
 #include "client.hpp"
 
+#include <algorithm>
+
 #include <cmath>
 #include <cstring>
 #include <thread>
@@ -125,6 +127,25 @@ void parallel_for(size_t count, int threads, F fn) {
 
 void ClientKey::encrypt_bit_at(uint64_t bit, uint64_t index, uint64_t *out) const {
     lwe_encrypt(seed.data(), ENCRYPT, index, glwe_sk.data(), p.K(), encode_bit(bit), p.lwe_std, out);
+}
+
+void ClientKey::encrypt_small_bit_at(uint64_t bit, uint64_t index, uint64_t *out) const {
+    lwe_encrypt(seed.data(), ENCRYPT, index, lwe_sk.data(), p.n, encode_bit(bit), p.lwe_std, out);
+}
+
+uint64_t ClientKey::phase_small(const uint64_t *ct) const {
+    uint64_t s = 0;
+    for (int i = 0; i < p.n; i++) s += ct[i] * lwe_sk[i];
+    return ct[p.n] - s;
+}
+
+void ClientKey::encrypt_int_at(uint64_t value, uint64_t index, uint64_t *out) const {
+    lwe_encrypt(seed.data(), ENCRYPT_INT, index, glwe_sk.data(), p.K(), (value & 255) << 56, p.glwe_std, out);
+}
+
+void generate_lut_without_padding(int N, const uint64_t *f_table, uint64_t *out) {
+    const int size = std::max(N, 256);
+    for (int i = 0; i < size; i++) out[i] = (f_table[i & 255] & 255) << 56;
 }
 
 uint64_t ClientKey::phase(const uint64_t *ct) const {

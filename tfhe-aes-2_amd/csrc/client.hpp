@@ -35,7 +35,7 @@ class ChaChaStream {
 };
 
 // Keygen stream purposes (DESIGN.md keygen spec).
-enum Purpose : uint64_t { LWE_SK = 1, GLWE_SK = 2, KSK = 3, BSK = 4, PFPKSK = 5, ENCRYPT = 6 };
+enum Purpose : uint64_t { LWE_SK = 1, GLWE_SK = 2, KSK = 3, BSK = 4, PFPKSK = 5, ENCRYPT = 6, ENCRYPT_INT = 7 };
 constexpr uint64_t kCtStride = 1ull << 24;
 
 inline uint64_t encode_bit(uint64_t bit) { return bit << 63; }
@@ -60,6 +60,26 @@ struct ClientKey {
     void encrypt_bit_at(uint64_t bit, uint64_t index, uint64_t *out) const;
     uint64_t phase(const uint64_t *ct) const;
     uint64_t decrypt_bit(const uint64_t *ct) const { return decode_bit(phase(ct)); }
+
+    // 8-bit model (shortint_woppbs_8bit.rs:196-225): bits are LWEs under the SMALL key [n+1]
+    void encrypt_small_bit_at(uint64_t bit, uint64_t index, uint64_t *out) const;
+    uint64_t phase_small(const uint64_t *ct) const;
+    uint64_t decrypt_small_bit(const uint64_t *ct) const { return decode_bit(phase_small(ct)); }
+    // shortint encrypt_without_padding / decrypt_without_padding (message modulus 256, carry 1):
+    // big-key LWE of m * 2^56 with glwe noise (the FullWidthCiphertext of the 8-bit model)
+    void encrypt_int_at(uint64_t value, uint64_t index, uint64_t *out) const;
+    uint64_t decrypt_int(const uint64_t *ct) const { return ((phase(ct) + (1ull << 55)) >> 56) & 255; }
+    // bits of either model: big key (model 1) or small key (model 8)
+    size_t bit_len() const { return p.model == 8 ? p.small_len() : p.big_len(); }
+    void encrypt_model_bit_at(uint64_t bit, uint64_t index, uint64_t *out) const {
+        if (p.model == 8)
+            encrypt_small_bit_at(bit, index, out);
+        else
+            encrypt_bit_at(bit, index, out);
+    }
+    uint64_t decrypt_model_bit(const uint64_t *ct) const {
+        return p.model == 8 ? decrypt_small_bit(ct) : decrypt_bit(ct);
+    }
 };
 
 // generate_keys_with_params; threads = worker threads for the key material.
@@ -72,6 +92,10 @@ void generate_client_key(const Params &p, const uint8_t seed[32], ClientKey &ck)
 // generate_multivariate_luts: out [output_bits][N << tree_bits]
 size_t lut_small_len(int N, int input_bits);
 void generate_lut(int N, int input_bits, int output_bits, const uint64_t *f_table, uint64_t *out);
+
+// WopbsKey::generate_lut_without_padding for message modulus 256 (8-bit model,
+// shortint_woppbs_8bit.rs:262-265): out[i] = (f(i mod 256) mod 256) << 56, i < max(N, 256)
+void generate_lut_without_padding(int N, const uint64_t *f_table /*[256]*/, uint64_t *out);
 
 // Negacyclic FFT tables (twist, untwist, W_M) -- the spec shared with the kernels.
 struct FftTables {

@@ -67,6 +67,20 @@ class Engine {
     // FheContext::circuit_bootstrap over G groups: bits [G][n_in][K+1] -> [G][n_out][K+1]
     void circuit_bootstrap(const uint64_t *d_bits, size_t G, int n_in, const uint64_t *d_lut,
                            int n_out, uint64_t *d_out);
+    // circuit_bootstrap_boolean_vertical_packing on small-key bits (no keyswitch):
+    // [G][n_in][n+1] -> [G][n_out][K+1]  (8-bit model: WopbsKey::circuit_bootstrapping_vertical_packing)
+    void cbs_vp(const uint64_t *d_small_bits, size_t G, int n_in, const uint64_t *d_lut, int n_out,
+                uint64_t *d_out);
+    // tfhe wop_pbs::extract_bits: big-key [B][K+1] -> small-key bits [B][nbits][n+1], MSB first
+    // (8-bit model extract_bits_from_ciphertext, shortint_woppbs_8bit.rs:268-296)
+    void extract_bits(const uint64_t *d_in, size_t B, int delta_log, int nbits, uint64_t *d_out);
+    // Byte::bootstrap_with_lut (fhe_impls/shortint_woppbs_8bit.rs:37-42) over G bytes:
+    // [G][8][n+1] -> [G][8][n+1] through one 8-bit int ciphertext per byte
+    void bootstrap_bytes8(const uint64_t *d_bytes, size_t G, const uint64_t *d_lut, uint64_t *d_out);
+    // fhe_sbox_pbs::encrypt_block_for_rounds over nb blocks of small-key bits (8-bit model):
+    // rk [44*32][n+1], blocks [nb][128][n+1]
+    void aes8_encrypt_blocks(const uint64_t *d_rk, const uint64_t *d_blocks, size_t nb, int rounds,
+                             uint64_t *d_out);
 
     // ---- AES driver (fhe_sbox_gal_mul_pbs::encrypt_block_for_rounds over many blocks) ----
     // rk [44*32][K+1] (expanded key words, word-major, MSB-first bits), blocks [nb][128][K+1]
@@ -85,6 +99,9 @@ class Engine {
 
     const uint64_t *lut_galmul() const { return d_lut24_; }  // 8 -> 24 (S, 2S', 3S')
     const uint64_t *lut_sbox() const { return d_lut8_; }     // 8 -> 8 SBOX
+    // 8-bit model LUTs without padding (SBOX, identity), [N]
+    const uint64_t *lut8_sbox() const { return d_wlut_sbox_; }
+    const uint64_t *lut8_identity() const { return d_wlut_id_; }
 
   private:
     void init_common();
@@ -102,6 +119,14 @@ class Engine {
     cplx *d_twist_ = nullptr, *d_untwist_ = nullptr, *d_w_ = nullptr;
     uint64_t *d_lut_shift_ = nullptr;  // per cbs level: trivial GLWE with body = -alpha
     uint64_t *d_lut24_ = nullptr, *d_lut8_ = nullptr;
+    uint64_t *d_wlut_sbox_ = nullptr, *d_wlut_id_ = nullptr;  // 8-bit model
+    uint64_t *d_lut_x_ = nullptr;                             // extract_bits accumulators [nbits][glwe]
+    int lut_x_delta_ = -1, lut_x_bits_ = 0;
+    uint64_t *d_xbuf_ = nullptr, *d_xsh_ = nullptr, *d_xks_ = nullptr, *d_xpbs_ = nullptr, *d_ints_ = nullptr;
+    size_t cap_xbuf_ = 0, cap_xsh_ = 0, cap_xks_ = 0, cap_xpbs_ = 0, cap_ints_ = 0;
+    int8_t mix_idx_[32][8] = {};
+    void cbs_vp_stages(const uint64_t *d_small_bits, size_t G, int n_in, const uint64_t *d_lut, int n_out,
+                       uint64_t *d_out);
     // scratch
     uint64_t *d_small_ = nullptr, *d_big_ = nullptr, *d_ggsw_ = nullptr, *d_state_ = nullptr,
              *d_muls_ = nullptr;

@@ -48,65 +48,71 @@ __device__ void ext_product_step(uint64_t *__restrict__ acc, cplx *__restrict__ 
     constexpr int M = N / 2;
     constexpr int R = FftPlan<M>::R, P = FftPlan<M>::P, TPJ = M / R;
     const int tid = threadIdx.x;
-    const int rows = (k + 1) * levels;
-
-    // ---- forward pass 0: rotated difference, decomposition, twist, DFT_R, twiddles ----
-    for (int jt = tid; jt < rows * TPJ; jt += blockDim.x) {
-        const int r = jt / TPJ, u = jt - r * TPJ;
-        const int p = r % (k + 1), lev = r / (k + 1) + 1;
-        const uint64_t *poly = acc + p * N;
-        cplx v[R];
-#pragma unroll
-        for (int m = 0; m < R; m++) {
-            const int j = u + m * TPJ;
-            const uint64_t d0 = rotated_coeff(poly, j, e, N) - poly[j];
-            const uint64_t d1 = rotated_coeff(poly, j + M, e, N) - poly[j + M];
-            const double x0 = (double)decomp_digit(d0, base_log, levels, lev);
-            const double x1 = (double)decomp_digit(d1, base_log, levels, lev);
-            const cplx t = twist[j];
-            v[m] = {fma(x0, t.re, -(x1 * t.im)), fma(x0, t.im, x1 * t.re)};
-        }
-        dft<R, M, false>(v, w);
-        cplx *dst = X + r * M;
-#pragma unroll
-        for (int kk = 0; kk < R; kk++) dst[u + kk * TPJ] = (u * kk) ? cmul(v[kk], w[u * kk]) : v[kk];
-    }
-    __syncthreads();
-    // ---- forward passes 1..P-1 ----
-    int L = TPJ / R;
-#pragma unroll
-    for (int s = 1; s < P; s++, L /= R) {
-        for (int jt = tid; jt < rows * TPJ; jt += blockDim.x) {
-            const int r = jt / TPJ, t = jt - r * TPJ;
-            const int g = t / L, u = t - g * L;
-            cplx *base = X + r * M + g * R * L + u;
+    // One decomposition level at a time (finest first): X holds that level's k+1 spectra and Y the
+    // running MAC, so LDS does not grow with the level count (pbs_l = 6 for the 8-bit model).
+    for (int lev = levels; lev >= 1; lev--) {
+        // ---- forward pass 0: rotated difference, decomposition, twist, DFT_R, twiddles ----
+        for (int jt = tid; jt < (k + 1) * TPJ; jt += blockDim.x) {
+            const int p = jt / TPJ, u = jt - p * TPJ;
+            const uint64_t *poly = acc + p * N;
             cplx v[R];
 #pragma unroll
-            for (int m = 0; m < R; m++) v[m] = base[m * L];
+            for (int m = 0; m < R; m++) {
+                const int j = u + m * TPJ;
+                const uint64_t d0 = rotated_coeff(poly, j, e, N) - poly[j];
+                const uint64_t d1 = rotated_coeff(poly, j + M, e, N) - poly[j + M];
+                const double x0 = (double)decomp_digit(d0, base_log, levels, lev);
+                const double x1 = (double)decomp_digit(d1, base_log, levels, lev);
+                const cplx t = twist[j];
+                v[m] = {fma(x0, t.re, -(x1 * t.im)), fma(x0, t.im, x1 * t.re)};
+            }
             dft<R, M, false>(v, w);
-            const int step = M / (R * L);
+            cplx *dst = X + p * M;
 #pragma unroll
-            for (int kk = 0; kk < R; kk++) base[kk * L] = (u * kk) ? cmul(v[kk], w[u * kk * step]) : v[kk];
+            for (int kk = 0; kk < R; kk++) dst[u + kk * TPJ] = (u * kk) ? cmul(v[kk], w[u * kk]) : v[kk];
         }
         __syncthreads();
-    }
-    // ---- pointwise multiply-accumulate with the GGSW (fixed fma order) ----
-    for (int idx = tid; idx < (k + 1) * M; idx += blockDim.x) {
-        const int c = idx / M, f = idx - c * M;
-        double re = 0.0, im = 0.0;
-        for (int lev = levels; lev >= 1; lev--)
+        // ---- forward passes 1..P-1 ----
+        int L = TPJ / R;
+#pragma unroll
+        for (int s = 1; s < P; s++, L /= R) {
+            for (int jt = tid; jt < (k + 1) * TPJ; jt += blockDim.x) {
+                const int r = jt / TPJ, t = jt - r * TPJ;
+                const int g = t / L, u = t - g * L;
+                cplx *base = X + r * M + g * R * L + u;
+                cplx v[R];
+#pragma unroll
+                for (int m = 0; m < R; m++) v[m] = base[m * L];
+                dft<R, M, false>(v, w);
+                const int step = M / (R * L);
+#pragma unroll
+                for (int kk = 0; kk < R; kk++) base[kk * L] = (u * kk) ? cmul(v[kk], w[u * kk * step]) : v[kk];
+            }
+            __syncthreads();
+        }
+        // ---- pointwise multiply-accumulate with this level's GGSW rows (fixed fma order:
+        //      level descending, row ascending, as in the oracle) ----
+        for (int idx = tid; idx < (k + 1) * M; idx += blockDim.x) {
+            const int c = idx / M, f = idx - c * M;
+            double re = 0.0, im = 0.0;
+            if (lev != levels) {
+                re = Y[c * M + f].re;
+                im = Y[c * M + f].im;
+            }
             for (int p = 0; p <= k; p++) {
                 const int r = (lev - 1) * (k + 1) + p;
-                const cplx x = X[r * M + f];
+                const cplx x = X[p * M + f];
                 const cplx g = ggsw[((size_t)r * (k + 1) + c) * M + f];
                 re = fma(x.re, g.re, re);
                 re = fma(-x.im, g.im, re);
                 im = fma(x.re, g.im, im);
                 im = fma(x.im, g.re, im);
             }
-        Y[c * M + f] = {re, im};
+            Y[c * M + f] = {re, im};
+        }
+        __syncthreads();
     }
-    __syncthreads();
+    int L;
     // ---- inverse passes P-1..1 (DIT) ----
     L = 1;
 #pragma unroll
@@ -169,7 +175,7 @@ __global__ void __launch_bounds__(kThreads) pbs_kernel(const uint64_t *__restric
     extern __shared__ __align__(16) unsigned char smem[];
     uint64_t *acc = reinterpret_cast<uint64_t *>(smem);
     cplx *X = reinterpret_cast<cplx *>(acc + (k + 1) * N);
-    cplx *Y = X + (k + 1) * levels * M;
+    cplx *Y = X + (k + 1) * M;
     const uint64_t *in = lwe_in + (size_t)blockIdx.x * (n + 1);
     const int bt = mod_switch(in[n] + body_add, logN);
     const int e0 = (2 * N - (bt % (2 * N))) % (2 * N);  // X^{-b~}
@@ -202,7 +208,7 @@ __global__ void __launch_bounds__(kThreads) vp_kernel(const cplx *__restrict__ g
     extern __shared__ __align__(16) unsigned char smem[];
     uint64_t *acc = reinterpret_cast<uint64_t *>(smem);
     cplx *X = reinterpret_cast<cplx *>(acc + (k + 1) * N);
-    cplx *Y = X + (k + 1) * levels * M;
+    cplx *Y = X + (k + 1) * M;
     const int g = blockIdx.x / n_out, jout = blockIdx.x - g * n_out;
     for (int t = threadIdx.x; t < (k + 1) * N; t += blockDim.x) acc[t] = t < k * N ? 0 : lut[(size_t)jout * N + (t - k * N)];
     __syncthreads();
@@ -406,6 +412,60 @@ __global__ void lwe_add_kernel(uint64_t *__restrict__ a, const uint64_t *__restr
         a[t] += b[t];
 }
 
+// ---------------------------------------------------------------------------------------------
+// 8-bit model helpers (shortint_woppbs_8bit.rs / fhe_sbox_pbs.rs)
+// ---------------------------------------------------------------------------------------------
+__global__ void lwe_shl_kernel(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t count, int shift) {
+    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < count; t += (size_t)gridDim.x * blockDim.x)
+        out[t] = in[t] << shift;
+}
+
+__global__ void lwe_sub_kernel(uint64_t *__restrict__ a, const uint64_t *__restrict__ b, size_t count) {
+    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < count; t += (size_t)gridDim.x * blockDim.x)
+        a[t] -= b[t];
+}
+
+// dst[r * dst_stride + j] = src[r * len + j]
+__global__ void copy_rows_kernel(const uint64_t *__restrict__ src, uint64_t *__restrict__ dst, size_t rows, int len,
+                                 size_t dst_stride) {
+    const size_t total = rows * (size_t)len;
+    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = t / len, j = t - r * len;
+        dst[r * dst_stride + j] = src[t];
+    }
+}
+
+// ShiftRows + MixColumns (fhe_sbox_pbs.rs:33-73: gf_256_mul as shifts and XORs of bits, i.e. LWE
+// additions) + AddRoundKey on small-key bits.  sb = SubBytes output [blk][16 bytes][8 bits][L];
+// T.idx[o][*] = the input bits (column-local, byte-major, MSB-first, -1 terminated) summed into
+// output bit o of a column (or_mix_column_terms in the oracle).
+struct MixTerms {
+    int8_t idx[32][8];
+};
+
+__global__ void aes8_mix_kernel(const uint64_t *__restrict__ sb, const uint64_t *__restrict__ rk_round,
+                                uint64_t *__restrict__ state, size_t nb, int L, MixTerms T) {
+    const size_t total = nb * 128 * (size_t)L;
+    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
+        const size_t coef = t % L;
+        const size_t ct = t / L;
+        const int bit = (int)(ct & 7);
+        const int pos = (int)((ct >> 3) & 15);
+        const size_t blk = ct >> 7;
+        const int c = pos >> 2, row = pos & 3, o = 8 * row + bit;
+        uint64_t acc = rk_round[(size_t)(pos * 8 + bit) * L + coef];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const int i = T.idx[o][q];
+            if (i < 0) break;
+            const int ri = i >> 3, bi = i & 7;
+            const int byte = 4 * ((c + ri) & 3) + ri;  // ShiftRows: state[ri][c] = sb[ri][(c + ri) % 4]
+            acc += sb[((blk * 16 + byte) * 8 + bi) * (size_t)L + coef];
+        }
+        state[t] = acc;
+    }
+}
+
 unsigned grid_for(size_t total) { return (unsigned)std::min<size_t>((total + kThreads - 1) / kThreads, 65536); }
 
 constexpr int kBrC = 3;  // ciphertexts per workgroup in the batched N=512 blind rotation
@@ -422,7 +482,8 @@ br512::W16 make_w16(const double *w) {
 
 template <int N>
 size_t br_lds_bytes(int k, int levels) {
-    return (size_t)(k + 1) * N * 8 + (size_t)(k + 1) * levels * (N / 2) * 16 + (size_t)(k + 1) * (N / 2) * 16;
+    (void)levels;  // ext_product_step works one level at a time
+    return (size_t)(k + 1) * N * 8 + 2 * (size_t)(k + 1) * (N / 2) * 16;
 }
 
 }  // namespace
@@ -482,6 +543,31 @@ void Engine::init_common() {
     d_lut8_ = static_cast<uint64_t *>(alloc(l8.size() * 8));
     HIPC(hipMemcpy(d_lut24_, l24.data(), l24.size() * 8, hipMemcpyHostToDevice));
     HIPC(hipMemcpy(d_lut8_, l8.data(), l8.size() * 8, hipMemcpyHostToDevice));
+    if (p_.model == 8) {
+        // 8-bit model: SBOX / identity LUTs without padding (fhe_impls/shortint_woppbs_8bit.rs:17-35)
+        std::vector<uint64_t> fs(256), fi(256), ws(std::max(p_.N, 256)), wi(std::max(p_.N, 256));
+        for (int x = 0; x < 256; x++) {
+            fs[x] = kSbox[x];
+            fi[x] = (uint64_t)x;
+        }
+        generate_lut_without_padding(p_.N, fs.data(), ws.data());
+        generate_lut_without_padding(p_.N, fi.data(), wi.data());
+        d_wlut_sbox_ = static_cast<uint64_t *>(alloc(ws.size() * 8));
+        d_wlut_id_ = static_cast<uint64_t *>(alloc(wi.size() * 8));
+        HIPC(hipMemcpy(d_wlut_sbox_, ws.data(), ws.size() * 8, hipMemcpyHostToDevice));
+        HIPC(hipMemcpy(d_wlut_id_, wi.data(), wi.size() * 8, hipMemcpyHostToDevice));
+        int terms[32][32];
+        mix_column_terms(terms);
+        for (int o = 0; o < 32; o++) {
+            int q = 0;
+            for (int i = 0; i < 32; i++)
+                for (int c = 0; c < terms[o][i]; c++) {
+                    if (q >= 8) throw std::runtime_error("MixColumns network: more than 8 terms per bit");
+                    mix_idx_[o][q++] = (int8_t)i;
+                }
+            for (; q < 8; q++) mix_idx_[o][q] = -1;
+        }
+    }
     // batched N=512 blind rotation (br512.hpp); TAE_BR_V1=1 forces the one-ciphertext kernels
     const char *v1 = getenv("TAE_BR_V1");
     batched512_ = p_.N == 512 && p_.k == 4 && !(v1 && v1[0] == '1');
@@ -599,7 +685,8 @@ Engine::~Engine() {
     for (void *q : {(void *)d_bsk_f_, (void *)d_twist_, (void *)d_untwist_, (void *)d_w_, (void *)d_lut_shift_,
                     (void *)d_lut24_, (void *)d_lut8_, (void *)d_small_, (void *)d_big_, (void *)d_ggsw_,
                     (void *)d_ggsw_f_, (void *)d_state_, (void *)d_muls_, (void *)d_pf_bt_, (void *)d_ks_bt_,
-                    (void *)d_digits_})
+                    (void *)d_digits_, (void *)d_wlut_sbox_, (void *)d_wlut_id_, (void *)d_lut_x_, (void *)d_xbuf_,
+                    (void *)d_xsh_, (void *)d_xks_, (void *)d_xpbs_, (void *)d_ints_})
         if (q) hipFree(q);
     for (auto &e : ev_) hipEventDestroy(e);
     hipStreamDestroy(stream_);
@@ -757,8 +844,26 @@ void Engine::circuit_bootstrap(const uint64_t *d_bits, size_t G, int n_in, const
     if (timing_) HIPC(hipEventRecord(ev_[0], stream_));
     keyswitch(d_bits, d_small_, bits);
     if (timing_) HIPC(hipEventRecord(ev_[1], stream_));
+    cbs_vp_stages(d_small_, G, n_in, d_lut, n_out, d_out);
+}
+
+void Engine::cbs_vp(const uint64_t *d_small_bits, size_t G, int n_in, const uint64_t *d_lut, int n_out,
+                    uint64_t *d_out) {
+    reserve(G * n_in, G * n_out);
+    if (timing_) {
+        HIPC(hipEventRecord(ev_[0], stream_));
+        HIPC(hipEventRecord(ev_[1], stream_));
+    }
+    cbs_vp_stages(d_small_bits, G, n_in, d_lut, n_out, d_out);
+}
+
+// circuit_bootstrap_boolean per bit and level (homomorphic_shift_boolean PBS + k+1 PFKS into the
+// GGSW rows of that level), GGSW to the Fourier domain, vertical packing
+void Engine::cbs_vp_stages(const uint64_t *d_small_bits, size_t G, int n_in, const uint64_t *d_lut, int n_out,
+                           uint64_t *d_out) {
+    const size_t bits = G * n_in;
     for (int lev = 1; lev <= p_.cbs_l; lev++) {
-        pbs_shift_boolean(d_small_, d_big_, bits, lev);
+        pbs_shift_boolean(d_small_bits, d_big_, bits, lev);
         if (timing_ && lev == p_.cbs_l) HIPC(hipEventRecord(ev_[2], stream_));
         pfks_into_ggsw(d_big_, d_ggsw_, bits, lev);
     }
@@ -777,6 +882,81 @@ void Engine::circuit_bootstrap(const uint64_t *d_bits, size_t G, int n_in, const
         HIPC(hipEventElapsedTime(&ms, ev_[4], ev_[5])); times_.vertical_packing += ms;
         times_.pbs_launches += p_.cbs_l;
     }
+}
+
+void Engine::extract_bits(const uint64_t *d_in, size_t B, int delta_log, int nbits, uint64_t *d_out) {
+    if (!B) return;
+    if (nbits < 1 || delta_log < 1 || delta_log + nbits > 64) throw std::runtime_error("extract_bits: bad bit range");
+    const size_t L = p_.big_len(), S = p_.small_len(), glwe = p_.glwe_len();
+    if (lut_x_delta_ != delta_log || lut_x_bits_ < nbits) {
+        // accumulators: trivial GLWE with body -alpha, alpha = 2^(delta_log - 1 + bit_idx)
+        std::vector<uint64_t> luts((size_t)nbits * glwe, 0);
+        for (int b = 0; b < nbits; b++) {
+            const uint64_t alpha = 1ull << (delta_log - 1 + b);
+            for (int j = 0; j < p_.N; j++) luts[(size_t)b * glwe + (size_t)p_.k * p_.N + j] = 0 - alpha;
+        }
+        if (d_lut_x_) HIPC(hipFree(d_lut_x_));
+        d_lut_x_ = static_cast<uint64_t *>(alloc(luts.size() * 8));
+        HIPC(hipMemcpy(d_lut_x_, luts.data(), luts.size() * 8, hipMemcpyHostToDevice));
+        lut_x_delta_ = delta_log;
+        lut_x_bits_ = nbits;
+    }
+    grow(d_xbuf_, cap_xbuf_, B * L);
+    grow(d_xsh_, cap_xsh_, B * L);
+    grow(d_xks_, cap_xks_, B * S);
+    grow(d_xpbs_, cap_xpbs_, B * L);
+    HIPC(hipMemcpyAsync(d_xbuf_, d_in, B * L * 8, hipMemcpyDeviceToDevice, stream_));
+    for (int bit_idx = 0; bit_idx < nbits; bit_idx++) {
+        // shift the extracted bit to the MSB, keyswitch: that is the output bit (LSB first, stored
+        // from the end so that the list is MSB first)
+        lwe_shl_kernel<<<grid_for(B * L), kThreads, 0, stream_>>>(d_xbuf_, d_xsh_, B * L, 64 - delta_log - bit_idx - 1);
+        HIPC(hipGetLastError());
+        keyswitch(d_xsh_, d_xks_, B);
+        copy_rows_kernel<<<grid_for(B * S), kThreads, 0, stream_>>>(d_xks_, d_out + (size_t)(nbits - 1 - bit_idx) * S, B,
+                                                                  (int)S, (size_t)nbits * S);
+        HIPC(hipGetLastError());
+        if (bit_idx == nbits - 1) break;
+        // PBS of (ks + q/4) with accumulator -alpha, + alpha: an encryption of the bit at alpha * 2;
+        // subtract it from the input to clear that bit
+        const uint64_t alpha = 1ull << (delta_log - 1 + bit_idx);
+        bootstrap(d_xks_, d_lut_x_ + (size_t)bit_idx * glwe, d_xpbs_, B, 1ull << 62, alpha);
+        lwe_sub_kernel<<<grid_for(B * L), kThreads, 0, stream_>>>(d_xbuf_, d_xpbs_, B * L);
+        HIPC(hipGetLastError());
+    }
+}
+
+void Engine::bootstrap_bytes8(const uint64_t *d_bytes, size_t G, const uint64_t *d_lut, uint64_t *d_out) {
+    if (!G) return;
+    grow(d_ints_, cap_ints_, G * p_.big_len());
+    cbs_vp(d_bytes, G, 8, d_lut, 1, d_ints_);
+    extract_bits(d_ints_, G, 56, 8, d_out);
+}
+
+void Engine::aes8_encrypt_blocks(const uint64_t *d_rk, const uint64_t *d_blocks, size_t nb, int rounds,
+                                 uint64_t *d_out) {
+    if (!nb) return;
+    if (p_.model != 8) throw std::runtime_error("aes8_encrypt_blocks needs the 8-bit model parameters");
+    if (rounds < 1 || rounds > 10) throw std::runtime_error("rounds must be in 1..=10");
+    const int L = (int)p_.small_len();
+    const size_t state_len = nb * 128 * (size_t)L;
+    times_ = StageTimes{};
+    grow(d_state_, cap_state_, state_len);
+    grow(d_muls_, cap_muls_, state_len);
+    const size_t byte_stride = 8 * (size_t)L;
+    MixTerms T;
+    std::memcpy(T.idx, mix_idx_, sizeof(T.idx));
+    aes_ark0_kernel<<<grid_for(state_len), kThreads, 0, stream_>>>(d_blocks, d_rk, d_state_, nb, L);
+    HIPC(hipGetLastError());
+    for (int r = 1; r < rounds; r++) {
+        bootstrap_bytes8(d_state_, nb * 16, d_wlut_sbox_, d_muls_);
+        aes8_mix_kernel<<<grid_for(state_len), kThreads, 0, stream_>>>(d_muls_, d_rk + (size_t)16 * r * byte_stride,
+                                                                        d_state_, nb, L, T);
+        HIPC(hipGetLastError());
+    }
+    bootstrap_bytes8(d_state_, nb * 16, d_wlut_sbox_, d_muls_);
+    aes_final_kernel<<<grid_for(state_len), kThreads, 0, stream_>>>(d_muls_, d_rk + (size_t)160 * byte_stride, d_out,
+                                                                     nb, L);
+    HIPC(hipGetLastError());
 }
 
 void Engine::aes_encrypt_blocks(const uint64_t *d_rk, const uint64_t *d_blocks, size_t nb, int rounds,

@@ -32,6 +32,43 @@ const uint8_t kSbox[256] = {
     0xb0, 0x54, 0xbb, 0x16};
 const uint8_t kRcon[11] = {0x00, 0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80, 0x1B, 0x36};
 
+void gf_256_mul_bit_terms(uint8_t b, int terms[8][8]) {
+    int a[8][8] = {}, res[8][8] = {};
+    for (int i = 0; i < 8; i++) a[i][i] = 1;
+    for (int it = 0; it < 8; it++) {
+        if (b & 1)
+            for (int o = 0; o < 8; o++)
+                for (int i = 0; i < 8; i++) res[o][i] += a[o][i];
+        // Byte::shl_assign_1 (data_model.rs:45-49): bit 0 leaves, the rest rotate left, a trivial
+        // zero enters at bit 7; the leaving bit is XORed into bits 3, 4, 6, 7
+        int red[8];
+        for (int i = 0; i < 8; i++) red[i] = a[0][i];
+        for (int o = 0; o < 7; o++)
+            for (int i = 0; i < 8; i++) a[o][i] = a[o + 1][i];
+        for (int i = 0; i < 8; i++) a[7][i] = 0;
+        for (int tap : {3, 4, 6, 7})
+            for (int i = 0; i < 8; i++) a[tap][i] += red[i];
+        b >>= 1;
+    }
+    for (int o = 0; o < 8; o++)
+        for (int i = 0; i < 8; i++) terms[o][i] = res[o][i];
+}
+
+void mix_column_terms(int terms[32][32]) {
+    int g[4][8][8];
+    for (int m = 1; m <= 3; m++) gf_256_mul_bit_terms((uint8_t)m, g[m]);
+    for (int o = 0; o < 32; o++)
+        for (int i = 0; i < 32; i++) terms[o][i] = 0;
+    for (int r = 0; r < 4; r++)
+        for (int o = 0; o < 8; o++)
+            for (int x = 0; x < 8; x++) {
+                terms[8 * r + o][8 * r + x] += g[2][o][x];
+                terms[8 * r + o][8 * ((r + 3) % 4) + x] += g[1][o][x];
+                terms[8 * r + o][8 * ((r + 2) % 4) + x] += g[1][o][x];
+                terms[8 * r + o][8 * ((r + 1) % 4) + x] += g[3][o][x];
+            }
+}
+
 uint8_t gf_256_mul(uint8_t a, uint8_t b) {
     uint8_t res = 0;
     for (int i = 0; i < 8; i++) {
@@ -97,7 +134,7 @@ void BitCt::xor_assign(const BitCt &rhs) {
 BitCt Context::trivial(uint64_t bit) const {
     if (bit > 1) throw ModelError{TAE_E_ARG, "cleartext out of bounds: " + std::to_string(bit)};
     BitCt b;
-    b.ct.assign(params().big_len(), 0);
+    b.ct.assign(bit_len(), 0);
     b.ct.back() = encode_bit(bit);
     b.noise = NoiseLevel::trivial();
     b.max_noise_sq = params().max_noise_sq;
@@ -107,7 +144,9 @@ BitCt Context::trivial(uint64_t bit) const {
 BitCt Context::wrap(std::vector<uint64_t> ct, uint64_t noise_level_squared) const {
     BitCt b;
     b.ct = std::move(ct);
-    b.noise = NoiseLevel::with_noise_level(noise_level_squared, next_ct_id());
+    // 8-bit model: shortint NoiseLevel (additive, no component ids; shortint_woppbs_8bit.rs:94-163)
+    b.noise = params().model == 8 ? NoiseLevel{noise_level_squared, {}}
+                                  : NoiseLevel::with_noise_level(noise_level_squared, next_ct_id());
     b.max_noise_sq = params().max_noise_sq;
     return b;
 }
@@ -118,6 +157,16 @@ Lut Context::generate_lookup_table(int input_bits, int output_bits, const uint64
     Lut l;
     l.input_bits = input_bits;
     l.output_bits = output_bits;
+    if (params().model == 8) {
+        // 8-bit model: FheContext::generate_lookup_table (shortint_woppbs_8bit.rs:262-265) is a byte ->
+        // byte map through WopbsKey::generate_lut_without_padding (one polynomial, 2^56 scale)
+        if (input_bits != 8 || output_bits != 8)
+            throw ModelError{TAE_E_PARAM, "the 8-bit model's lookup tables map 8 bits to 8 bits"};
+        l.small_len = (size_t)std::max(params().N, 256);
+        l.data.assign(l.small_len, 0);
+        generate_lut_without_padding(params().N, f_values, l.data.data());
+        return l;
+    }
     l.small_len = lut_small_len(params().N, input_bits);
     l.data.assign(l.small_len * output_bits, 0);
     generate_lut(params().N, input_bits, output_bits, f_values, l.data.data());
@@ -138,9 +187,58 @@ struct DevBuf {
 };
 }  // namespace
 
+// Run fn(d_in, d_out, d_lut) on the engine stream with host staging unless device_mem.
+template <class F>
+void Context::run8(const uint64_t *in, size_t in_len, uint64_t *out, size_t out_len, bool device_mem, F fn,
+                   const Lut *lut) {
+    std::lock_guard<std::mutex> g(mu_);
+    hip_check(hipSetDevice(engine_->device()), "hipSetDevice");
+    std::unique_ptr<DevBuf> d_lut;
+    if (lut) {
+        d_lut = std::make_unique<DevBuf>(lut->data.size() * 8);
+        hip_check(hipMemcpyAsync(d_lut->p, lut->data.data(), lut->data.size() * 8, hipMemcpyHostToDevice,
+                                 engine_->stream()),
+                  "lut upload");
+    }
+    const uint64_t *dl = d_lut ? d_lut->as<uint64_t>() : nullptr;
+    if (device_mem) {
+        fn(in, out, dl);
+        engine_->synchronize();
+        return;
+    }
+    DevBuf d_in(in_len * 8), d_out(out_len * 8);
+    hip_check(hipMemcpyAsync(d_in.p, in, in_len * 8, hipMemcpyHostToDevice, engine_->stream()), "upload");
+    fn(d_in.as<uint64_t>(), d_out.as<uint64_t>(), dl);
+    hip_check(hipMemcpyAsync(out, d_out.p, out_len * 8, hipMemcpyDeviceToHost, engine_->stream()), "download");
+    engine_->synchronize();
+}
+
+void Context::bootstrap_from_bits_raw(const uint64_t *bits, size_t groups, const Lut &lut, uint64_t *out,
+                                      bool device_mem) {
+    if (params().model != 8) throw ModelError{TAE_E_PARAM, "bootstrap_from_bits belongs to the 8-bit model"};
+    if (lut.input_bits != 8) throw ModelError{TAE_E_ARG, "bootstrap_from_bits needs an 8-bit LUT"};
+    run8(bits, groups * 8 * bit_len(), out, groups * params().big_len(), device_mem,
+         [&](const uint64_t *in, uint64_t *o, const uint64_t *d_lut) { engine_->cbs_vp(in, groups, 8, d_lut, 1, o); },
+         &lut);
+}
+
+void Context::extract_bits_raw(const uint64_t *ints, size_t groups, uint64_t *out, bool device_mem) {
+    if (params().model != 8) throw ModelError{TAE_E_PARAM, "extract_bits_from_ciphertext belongs to the 8-bit model"};
+    run8(ints, groups * params().big_len(), out, groups * 8 * bit_len(), device_mem,
+         [&](const uint64_t *in, uint64_t *o, const uint64_t *) { engine_->extract_bits(in, groups, 56, 8, o); },
+         nullptr);
+}
+
 void Context::circuit_bootstrap_raw(const uint64_t *bits, size_t groups, int n_in, const Lut &lut, uint64_t *out,
                                     bool device_mem) {
     if (n_in != lut.input_bits) throw ModelError{TAE_E_ARG, "number of input bits does not match the LUT"};
+    if (params().model == 8) {
+        // Byte::bootstrap_with_lut (fhe_impls/shortint_woppbs_8bit.rs:37-42): bits [G][8][n+1] -> [G][8][n+1]
+        run8(bits, groups * 8 * bit_len(), out, groups * 8 * bit_len(), device_mem,
+             [&](const uint64_t *in, uint64_t *o, const uint64_t *d_lut) { engine_->bootstrap_bytes8(in, groups, d_lut, o); },
+             &lut);
+        return;
+    }
     if (lut.small_len != (size_t)params().N)
         throw ModelError{TAE_E_PARAM, "LUTs with input_bits > log2(N) need the CMux tree (not on device yet)"};
     std::lock_guard<std::mutex> g(mu_);
@@ -166,7 +264,20 @@ void Context::circuit_bootstrap_raw(const uint64_t *bits, size_t groups, int n_i
 
 // FheContext::circuit_bootstrap (shortint_woppbs_1bit.rs:292-336)
 std::vector<BitCt> Context::circuit_bootstrap(const std::vector<const BitCt *> &bits, const Lut &lut) {
-    const size_t L = params().big_len();
+    const size_t L = bit_len();
+    for (const BitCt *b : bits)
+        if (b->ct.size() != L) throw ModelError{TAE_E_ARG, "ciphertext size mismatch"};
+    if (params().model == 8) {
+        // Byte::bootstrap_with_lut: extract_bits outputs are BitCt::new (NOMINAL noise)
+        if (bits.size() != 8) throw ModelError{TAE_E_ARG, "the 8-bit model bootstraps whole bytes"};
+        std::vector<uint64_t> in8(8 * L), out8(8 * L);
+        for (size_t b = 0; b < 8; b++) std::memcpy(&in8[b * L], bits[b]->ct.data(), L * 8);
+        circuit_bootstrap_raw(in8.data(), 1, 8, lut, out8.data(), false);
+        std::vector<BitCt> res;
+        for (int j = 0; j < 8; j++)
+            res.push_back(wrap(std::vector<uint64_t>(out8.begin() + j * L, out8.begin() + (j + 1) * L), 1));
+        return res;
+    }
     std::vector<uint64_t> in(bits.size() * L), out((size_t)lut.output_bits * L);
     for (size_t b = 0; b < bits.size(); b++) std::memcpy(&in[b * L], bits[b]->ct.data(), L * 8);
     circuit_bootstrap_raw(in.data(), 1, (int)bits.size(), lut, out.data(), false);
@@ -220,9 +331,62 @@ std::vector<NoiseLevel> aes_noise_schedule(const std::vector<NoiseLevel> &rk, co
     return st;
 }
 
+// fhe_sbox_pbs::encrypt_block_for_rounds (:75-121) on metadata: SubBytes = bootstrap_with_lut
+// (outputs NOMINAL), MixColumns adds the network's terms, ARK the key bit.
+std::vector<NoiseLevel> aes8_noise_schedule(const std::vector<NoiseLevel> &rk, const std::vector<NoiseLevel> &block,
+                                            int rounds, uint64_t max) {
+    int terms[32][32];
+    mix_column_terms(terms);
+    auto key_bit = [&](int word, int byte, int bit) -> const NoiseLevel & { return rk[(word * 4 + byte) * 8 + bit]; };
+    std::vector<NoiseLevel> st = block;
+    for (int c = 0; c < 4; c++)
+        for (int r = 0; r < 4; r++)
+            for (int b = 0; b < 8; b++) st[(4 * c + r) * 8 + b].add_assign(key_bit(c, r, b), max);
+    const NoiseLevel nominal{1, {}};
+    for (int round = 1; round <= rounds; round++) {
+        const bool last = round == rounds;
+        for (int c = 0; c < 4; c++)
+            for (int o = 0; o < 32; o++) {
+                NoiseLevel v{0, {}};
+                if (last) {
+                    v = nominal;
+                } else {
+                    for (int i = 0; i < 32; i++)
+                        for (int t = 0; t < terms[o][i]; t++) v.add_assign(nominal, max);
+                }
+                v.add_assign(key_bit(last ? 40 + c : 4 * round + c, o / 8, o % 8), max);
+                st[(4 * c + o / 8) * 8 + o % 8] = std::move(v);
+            }
+    }
+    return st;
+}
+
 void Context::aes_encrypt_blocks_raw(const uint64_t *rk, const uint64_t *blocks, size_t n_blocks, int rounds,
                                      uint64_t *out, bool device_mem) {
     if (rounds < 1 || rounds > kAesRounds) throw ModelError{TAE_E_PARAM, "rounds must be in 1..=10"};
+    if (params().model == 8) {
+        {
+            std::vector<NoiseLevel> krk(44 * 32, NoiseLevel{1, {}}), kbl(128, NoiseLevel{1, {}});
+            aes8_noise_schedule(krk, kbl, rounds, params().max_noise_sq);
+        }
+        const size_t S = bit_len();
+        std::lock_guard<std::mutex> g(mu_);
+        hip_check(hipSetDevice(engine_->device()), "hipSetDevice");
+        if (device_mem) {
+            engine_->aes8_encrypt_blocks(rk, blocks, n_blocks, rounds, out);
+            engine_->synchronize();
+            return;
+        }
+        DevBuf d_rk(44 * 32 * S * 8), d_in(n_blocks * 128 * S * 8), d_out(n_blocks * 128 * S * 8);
+        hip_check(hipMemcpyAsync(d_rk.p, rk, 44 * 32 * S * 8, hipMemcpyHostToDevice, engine_->stream()), "upload rk");
+        hip_check(hipMemcpyAsync(d_in.p, blocks, n_blocks * 128 * S * 8, hipMemcpyHostToDevice, engine_->stream()),
+                  "upload blocks");
+        engine_->aes8_encrypt_blocks(d_rk.as<uint64_t>(), d_in.as<uint64_t>(), n_blocks, rounds, d_out.as<uint64_t>());
+        hip_check(hipMemcpyAsync(out, d_out.p, n_blocks * 128 * S * 8, hipMemcpyDeviceToHost, engine_->stream()),
+                  "download");
+        engine_->synchronize();
+        return;
+    }
     {
         // static validation of the fixed AES noise schedule for fresh inputs (noise^2 = 1)
         std::vector<NoiseLevel> krk(44 * 32), kbl(128);
@@ -254,14 +418,19 @@ std::vector<BitCt> Context::aes_encrypt_blocks(const std::vector<const BitCt *> 
     if (expanded_key.size() != 44 * 32) throw ModelError{TAE_E_ARG, "expanded key must be 44 words (1408 bits)"};
     if (blocks.size() != n_blocks * 128) throw ModelError{TAE_E_ARG, "blocks must be 128 bits each"};
     if (rounds < 1 || rounds > kAesRounds) throw ModelError{TAE_E_PARAM, "rounds must be in 1..=10"};
-    const size_t L = params().big_len();
+    const size_t L = bit_len();
+    for (const BitCt *b : expanded_key)
+        if (b->ct.size() != L) throw ModelError{TAE_E_ARG, "ciphertext size mismatch"};
+    for (const BitCt *b : blocks)
+        if (b->ct.size() != L) throw ModelError{TAE_E_ARG, "ciphertext size mismatch"};
     std::vector<NoiseLevel> krk(44 * 32);
     for (size_t i = 0; i < krk.size(); i++) krk[i] = expanded_key[i]->noise;
     std::vector<std::vector<NoiseLevel>> out_noise(n_blocks);
     for (size_t blk = 0; blk < n_blocks; blk++) {
         std::vector<NoiseLevel> kb(128);
         for (int i = 0; i < 128; i++) kb[i] = blocks[blk * 128 + i]->noise;
-        out_noise[blk] = aes_noise_schedule(krk, kb, rounds, params().max_noise_sq);
+        out_noise[blk] = params().model == 8 ? aes8_noise_schedule(krk, kb, rounds, params().max_noise_sq)
+                                             : aes_noise_schedule(krk, kb, rounds, params().max_noise_sq);
     }
     std::vector<uint64_t> rk(44 * 32 * L), in(n_blocks * 128 * L), out(n_blocks * 128 * L);
     for (size_t i = 0; i < 44 * 32; i++) std::memcpy(&rk[i * L], expanded_key[i]->ct.data(), L * 8);
@@ -272,7 +441,10 @@ std::vector<BitCt> Context::aes_encrypt_blocks(const std::vector<const BitCt *> 
         DevBuf d_rk(rk.size() * 8), d_in(in.size() * 8), d_out(out.size() * 8);
         hip_check(hipMemcpyAsync(d_rk.p, rk.data(), rk.size() * 8, hipMemcpyHostToDevice, engine_->stream()), "up");
         hip_check(hipMemcpyAsync(d_in.p, in.data(), in.size() * 8, hipMemcpyHostToDevice, engine_->stream()), "up");
-        engine_->aes_encrypt_blocks(d_rk.as<uint64_t>(), d_in.as<uint64_t>(), n_blocks, rounds, d_out.as<uint64_t>());
+        if (params().model == 8)
+            engine_->aes8_encrypt_blocks(d_rk.as<uint64_t>(), d_in.as<uint64_t>(), n_blocks, rounds, d_out.as<uint64_t>());
+        else
+            engine_->aes_encrypt_blocks(d_rk.as<uint64_t>(), d_in.as<uint64_t>(), n_blocks, rounds, d_out.as<uint64_t>());
         hip_check(hipMemcpyAsync(out.data(), d_out.p, out.size() * 8, hipMemcpyDeviceToHost, engine_->stream()), "dn");
         engine_->synchronize();
     }
@@ -290,6 +462,7 @@ std::vector<BitCt> Context::aes_encrypt_blocks(const std::vector<const BitCt *> 
 // (SubWord(RotWord) + Rcon when i%4 == 0), then every bit of word i is bootstrapped (identity LUT).
 std::vector<BitCt> Context::aes_key_schedule(const std::vector<const BitCt *> &key) {
     if (key.size() != 128) throw ModelError{TAE_E_ARG, "key must be 16 bytes (128 bits)"};
+    if (params().model == 8) return aes8_key_schedule(key);
     const size_t L = params().big_len();
     std::vector<BitCt> ek(44 * 32);
     for (int i = 0; i < 128; i++) ek[i] = *key[i];
@@ -332,6 +505,85 @@ std::vector<BitCt> Context::aes_key_schedule(const std::vector<const BitCt *> &k
             ek[i * 32 + t] = wrap(std::vector<uint64_t>(out.begin() + t * L, out.begin() + (t + 1) * L), 1);
     }
     return ek;
+}
+
+// fhe_sbox_pbs::key_schedule (:123-171) with the 8-bit model's ByteT (fhe_impls/shortint_woppbs_8bit.rs:17-42):
+// sub_word = sbox_substitute of each byte of RotWord(ek[i-1]); after every 4th word the four words
+// i-3..i are boot_word-ed (identity bootstrap_with_lut of each byte).
+std::vector<BitCt> Context::aes8_key_schedule(const std::vector<const BitCt *> &key) {
+    const size_t L = bit_len();
+    for (const BitCt *b : key)
+        if (b->ct.size() != L) throw ModelError{TAE_E_ARG, "ciphertext size mismatch"};
+    std::vector<BitCt> ek(44 * 32);
+    for (int i = 0; i < 128; i++) ek[i] = *key[i];
+    uint64_t ftab_sbox[256], ftab_id[256];
+    for (int x = 0; x < 256; x++) {
+        ftab_sbox[x] = kSbox[x];
+        ftab_id[x] = (uint64_t)x;
+    }
+    const Lut sbox = generate_lookup_table(8, 8, ftab_sbox);
+    const Lut ident = generate_lookup_table(8, 8, ftab_id);
+    auto boot = [&](std::vector<BitCt *> bits, const Lut &lut) {  // whole bytes, in place
+        const size_t nbytes = bits.size() / 8;
+        std::vector<uint64_t> in(bits.size() * L), out(bits.size() * L);
+        for (size_t t = 0; t < bits.size(); t++) std::memcpy(&in[t * L], bits[t]->ct.data(), L * 8);
+        circuit_bootstrap_raw(in.data(), nbytes, 8, lut, out.data(), false);
+        for (size_t t = 0; t < bits.size(); t++)
+            *bits[t] = wrap(std::vector<uint64_t>(out.begin() + t * L, out.begin() + (t + 1) * L), 1);
+    };
+    auto bit_at = [&](int word, int byte, int bit) -> BitCt & { return ek[(word * 4 + byte) * 8 + bit]; };
+    for (int i = 4; i < 44; i++) {
+        if (i % 4 == 0) {
+            std::vector<BitCt> rot(32);
+            std::vector<BitCt *> rp(32);
+            for (int byte = 0; byte < 4; byte++)
+                for (int b = 0; b < 8; b++) rot[byte * 8 + b] = bit_at(i - 1, (byte + 1) % 4, b);
+            for (int t = 0; t < 32; t++) rp[t] = &rot[t];
+            boot(rp, sbox);
+            for (int t = 0; t < 32; t++) {
+                BitCt v = ek[(i - 4) * 32 + t];
+                v.xor_assign(rot[t]);
+                ek[i * 32 + t] = std::move(v);
+            }
+            for (int b = 0; b < 8; b++) ek[i * 32 + b].xor_assign(trivial((kRcon[i / 4] >> (7 - b)) & 1));
+        } else {
+            for (int t = 0; t < 32; t++) {
+                BitCt v = ek[(i - 4) * 32 + t];
+                v.xor_assign(ek[(i - 1) * 32 + t]);
+                ek[i * 32 + t] = std::move(v);
+            }
+        }
+        if (i % 4 == 3) {
+            std::vector<BitCt *> ws(128);
+            for (int t = 0; t < 128; t++) ws[t] = &ek[(i - 3) * 32 + t];
+            boot(ws, ident);
+        }
+    }
+    return ek;
+}
+
+void Context::aes_key_schedule_raw(const uint64_t *key, uint64_t *expanded, bool device_mem) {
+    const size_t L = bit_len();
+    std::vector<uint64_t> hk(128 * L);
+    if (device_mem) {
+        hip_check(hipSetDevice(engine_->device()), "hipSetDevice");
+        hip_check(hipMemcpy(hk.data(), key, hk.size() * 8, hipMemcpyDeviceToHost), "download key");
+    } else {
+        std::memcpy(hk.data(), key, hk.size() * 8);
+    }
+    std::vector<BitCt> kb(128);
+    std::vector<const BitCt *> kp(128);
+    for (int i = 0; i < 128; i++) {
+        kb[i] = wrap(std::vector<uint64_t>(hk.begin() + i * L, hk.begin() + (i + 1) * L), 1);  // fresh
+        kp[i] = &kb[i];
+    }
+    const std::vector<BitCt> ek = aes_key_schedule(kp);
+    std::vector<uint64_t> he(44 * 32 * L);
+    for (size_t i = 0; i < ek.size(); i++) std::memcpy(&he[i * L], ek[i].ct.data(), L * 8);
+    if (device_mem)
+        hip_check(hipMemcpy(expanded, he.data(), he.size() * 8, hipMemcpyHostToDevice), "upload expanded key");
+    else
+        std::memcpy(expanded, he.data(), he.size() * 8);
 }
 
 }  // namespace tae

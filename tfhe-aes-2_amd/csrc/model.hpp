@@ -79,8 +79,20 @@ class Context {  // FheContext
     // raw arrays, fresh inputs; static noise-schedule validation
     void aes_encrypt_blocks_raw(const uint64_t *rk, const uint64_t *blocks, size_t n_blocks, int rounds,
                                 uint64_t *out, bool device_mem);
+    // raw key schedule (either model): key [128][bit_len] fresh bits -> [44*32][bit_len]
+    void aes_key_schedule_raw(const uint64_t *key, uint64_t *expanded, bool device_mem);
+
+    // ---- 8-bit model (src/tfhe/shortint_woppbs_8bit.rs, fhe_impls/shortint_woppbs_8bit.rs) ----
+    size_t bit_len() const { return params().model == 8 ? params().small_len() : params().big_len(); }
+    // FheContext::bootstrap_from_bits over G bytes: bits [G][8][n+1] -> int ciphertexts [G][K+1]
+    void bootstrap_from_bits_raw(const uint64_t *bits, size_t groups, const Lut &lut, uint64_t *out, bool device_mem);
+    // FheContext::extract_bits_from_ciphertext over G ints: [G][K+1] -> [G][8][n+1]
+    void extract_bits_raw(const uint64_t *ints, size_t groups, uint64_t *out, bool device_mem);
 
   private:
+    template <class F>
+    void run8(const uint64_t *in, size_t in_len, uint64_t *out, size_t out_len, bool device_mem, F fn, const Lut *lut);
+    std::vector<BitCt> aes8_key_schedule(const std::vector<const BitCt *> &key);
     std::unique_ptr<Engine> engine_;
     std::mutex mu_;
 };
@@ -89,5 +101,9 @@ class Context {  // FheContext
 // (per bit) or throws ModelError exactly where the reference would panic.
 std::vector<NoiseLevel> aes_noise_schedule(const std::vector<NoiseLevel> &rk, const std::vector<NoiseLevel> &block,
                                            int rounds, uint64_t max_noise_sq);
+// The same for fhe_sbox_pbs with the 8-bit model (additive shortint NoiseLevel, max 11; SubBytes
+// outputs are NOMINAL = 1).
+std::vector<NoiseLevel> aes8_noise_schedule(const std::vector<NoiseLevel> &rk, const std::vector<NoiseLevel> &block,
+                                            int rounds, uint64_t max_noise_level);
 
 }  // namespace tae

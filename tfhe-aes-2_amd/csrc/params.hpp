@@ -1,4 +1,4 @@
-// Parameter sets of the 1-bit WoP-PBS model.
+// Parameter sets of the 1-bit WoP-PBS model, and the 8-bit model's single set.
 // Reference: src/tfhe/shortint_woppbs_1bit/parameters.rs:29-205 (WopbsParameters +
 // max_noise_level_squared).  Default for the AES path: params_sqrd_lvl_64 (main.rs:82-83).
 #pragma once
@@ -17,7 +17,9 @@ struct Params {
     int cbs_l, cbs_b;
     int pfks_l, pfks_b;
     double lwe_std, glwe_std, pfks_std;
-    uint64_t max_noise_sq;
+    uint64_t max_noise_sq;  // 1-bit model: max noise^2; 8-bit model: shortint MaxNoiseLevel
+    int model = 1;          // 1: shortint_woppbs_1bit (bits under the big key); 8: shortint_woppbs_8bit
+                            //    (bits under the small key, bytes bootstrapped through an 8-bit int)
 
     int K() const { return k * N; }                    // big LWE dimension
     int M() const { return N / 2; }                    // Fourier coefficients per polynomial
@@ -32,7 +34,7 @@ struct Params {
     size_t cbs_ggsw_fourier_len() const { return (size_t)cbs_l * (k + 1) * (k + 1) * M(); }
 };
 
-enum ParamSet { SQRD_LVL_1 = 0, SQRD_LVL_4 = 1, SQRD_LVL_64 = 2, SQRD_LVL_256 = 3 };
+enum ParamSet { SQRD_LVL_1 = 0, SQRD_LVL_4 = 1, SQRD_LVL_64 = 2, SQRD_LVL_256 = 3, WOPPBS_8BIT = 4 };
 
 inline bool get_params(int id, Params &p) {
     switch (id) {
@@ -52,6 +54,12 @@ inline bool get_params(int id, Params &p) {
     case SQRD_LVL_256:  // parameters.rs:173-205
         p = {id, 665, 2, 1024, 4, 9, 6, 2, 1, 14, 3, 12,
              4.7280002450549286e-05, 3.162026630747649e-16, 3.162026630747649e-16, 256};
+        return true;
+    case WOPPBS_8BIT:  // src/tfhe/shortint_woppbs_8bit.rs:39-86 (message modulus 256, carry 1,
+                       // MaxNoiseLevel::new(11))
+        p = {id, 785, 2, 1024, 6, 7, 8, 2, 4, 6, 3, 12,
+             1.5140301927925663e-05, 0.00000000000000022148688116005568,
+             0.00000000000000022148688116005568, 11, 8};
         return true;
     default:
         return false;

@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("TAE_LIB_PATH") or os.path.join(_HERE, "libtfhe_aes_am
 TAE_OK, TAE_E_NOISE, TAE_E_INDEP, TAE_E_PARAM, TAE_E_HIP, TAE_E_ARG, TAE_E_NODEV = range(7)
 TAE_MEM_HOST, TAE_MEM_DEVICE = 0, 1
 PARAMS_SQRD_LVL_1, PARAMS_SQRD_LVL_4, PARAMS_SQRD_LVL_64, PARAMS_SQRD_LVL_256 = 0, 1, 2, 3
+PARAMS_WOPPBS_8BIT = 4  # shortint_woppbs_8bit.rs:39-86 (bits under the small key)
 
 # Every symbol include/tfhe_aes_gpu.h declares (checked by tests/test_capi_symbols.py).
 EXPORTED = [
@@ -27,7 +28,8 @@ EXPORTED = [
     "tae_circuit_bootstrap_raw", "tae_aes_encrypt_block_for_rounds", "tae_aes_encrypt_blocks",
     "tae_aes_key_schedule", "tae_aes_encrypt_blocks_raw", "tae_stage_keyswitch", "tae_stage_pbs_shift_boolean",
     "tae_stage_bootstrap", "tae_stage_pfks_ggsw", "tae_stage_ggsw_fourier", "tae_stage_vertical_packing",
-    "tae_synchronize", "tae_set_timing", "tae_last_stage_times",
+    "tae_synchronize", "tae_set_timing", "tae_last_stage_times", "tae_bit_len", "tae_encrypt_ints_raw",
+    "tae_decrypt_ints_raw", "tae_bootstrap_from_bits_raw", "tae_extract_bits_raw", "tae_aes_key_schedule_raw",
 ]
 
 
@@ -35,7 +37,7 @@ class TaeParams(C.Structure):
     _fields_ = [(n, C.c_int) for n in
                 ("n", "k", "N", "pbs_l", "pbs_b", "ks_l", "ks_b", "cbs_l", "cbs_b", "pfks_l", "pfks_b")] + [
         ("lwe_std", C.c_double), ("glwe_std", C.c_double), ("pfks_std", C.c_double),
-        ("max_noise_sq", C.c_uint64)]
+        ("max_noise_sq", C.c_uint64), ("model", C.c_int)]
 
     def as_dict(self) -> dict:
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -109,6 +111,12 @@ def lib() -> C.CDLL:
         "tae_stage_vertical_packing": ([vp, vp, sz, C.c_int, vp, C.c_int, vp, C.c_int], C.c_int),
         "tae_synchronize": ([vp], C.c_int), "tae_set_timing": ([vp, C.c_int], C.c_int),
         "tae_last_stage_times": ([vp, C.POINTER(C.c_float)], C.c_int),
+        "tae_bit_len": ([C.c_int, C.POINTER(sz)], C.c_int),
+        "tae_encrypt_ints_raw": ([vp, vp, sz, u64, vp], C.c_int),
+        "tae_decrypt_ints_raw": ([vp, vp, sz, vp], C.c_int),
+        "tae_bootstrap_from_bits_raw": ([vp, vp, sz, vp, vp, C.c_int], C.c_int),
+        "tae_extract_bits_raw": ([vp, vp, sz, vp, C.c_int], C.c_int),
+        "tae_aes_key_schedule_raw": ([vp, vp, vp, C.c_int], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -128,6 +136,12 @@ def get_params(param_set: int) -> dict:
     p = TaeParams()
     check(lib().tae_get_params(param_set, C.byref(p)))
     return p.as_dict()
+
+
+def bit_len(param_set: int) -> int:
+    n = C.c_size_t(0)
+    check(lib().tae_bit_len(param_set, C.byref(n)))
+    return n.value
 
 
 def device_count() -> int:

@@ -194,6 +194,25 @@ class ShortintWoppbs1BitSboxGalMulPbsAesEncrypt:
                                                C.c_void_p(d_out), N.TAE_MEM_DEVICE))
 
 
+    @staticmethod
+    def key_schedule_raw(ctx: FheContext, key: np.ndarray) -> np.ndarray:
+        """Host arrays: fresh key bits [128][L] -> expanded [1408][L] (L = ctx.lwe_size)."""
+        key = np.ascontiguousarray(key, dtype=np.uint64)
+        out = np.zeros((44 * 32, ctx.lwe_size), dtype=np.uint64)
+        check(lib().tae_aes_key_schedule_raw(ctx._h, key.ctypes.data_as(C.c_void_p), out.ctypes.data_as(C.c_void_p),
+                                             N.TAE_MEM_HOST))
+        return out
+
+
+class ShortintWoppbs8BitSboxPbsAesEncrypt(ShortintWoppbs1BitSboxGalMulPbsAesEncrypt):
+    """fhe_impls/shortint_woppbs_8bit.rs:44-64 -- fhe_sbox_pbs driver over the 8-bit model.
+
+    Same API; use a context of param set PARAMS_WOPPBS_8BIT (bits are small-key LWEs [n+1]).  SubBytes is
+    Byte::bootstrap_with_lut (CBS-VP of the 8 bits into one 8-bit int, then extract_bits), MixColumns is
+    leveled (gf_256_mul by bit shifts/XORs, fhe_sbox_pbs.rs:33-73).  The C-ABI dispatches on the model.
+    """
+
+
 def counter_blocks(iv: bytes, count: int) -> List[bytes]:
     """main.rs:108-115: block = iv (8 bytes) || ctr as u64 big-endian, ctr = 1..=count."""
     return [bytes(iv) + c.to_bytes(8, "big") for c in range(1, count + 1)]

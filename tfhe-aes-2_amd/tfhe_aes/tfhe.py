@@ -128,7 +128,8 @@ class FheContext:
         p = N.TaeParams()
         check(lib().tae_context_params(self._h, C.byref(p)))
         self.params = p.as_dict()
-        self.lwe_size = self.params["k"] * self.params["N"] + 1
+        self.lwe_size = N.bit_len(param_set)  # one bit: K+1 (1-bit model) or n+1 (8-bit model)
+        self.int_size = self.params["k"] * self.params["N"] + 1
 
     def __del__(self):
         try:
@@ -173,6 +174,23 @@ class FheContext:
                                               out.ctypes.data_as(C.c_void_p), N.TAE_MEM_HOST))
         return out
 
+    # ---- 8-bit model (shortint_woppbs_8bit.rs:268-336) ----
+    def bootstrap_from_bits_raw(self, bits: np.ndarray, lut: WopbsLUT) -> np.ndarray:
+        """FheContext::bootstrap_from_bits over bytes: [groups][8][n+1] -> int ciphertexts [groups][K+1]."""
+        bits = np.ascontiguousarray(bits, dtype=np.uint64)
+        out = np.zeros((bits.shape[0], self.int_size), dtype=np.uint64)
+        check(lib().tae_bootstrap_from_bits_raw(self._h, bits.ctypes.data_as(C.c_void_p), bits.shape[0], lut._h,
+                                                out.ctypes.data_as(C.c_void_p), N.TAE_MEM_HOST))
+        return out
+
+    def extract_bits_from_ciphertext_raw(self, ints: np.ndarray) -> np.ndarray:
+        """FheContext::extract_bits_from_ciphertext: [groups][K+1] -> [groups][8][n+1], MSB first."""
+        ints = np.ascontiguousarray(ints, dtype=np.uint64).reshape(-1, self.int_size)
+        out = np.zeros((ints.shape[0], 8, self.lwe_size), dtype=np.uint64)
+        check(lib().tae_extract_bits_raw(self._h, ints.ctypes.data_as(C.c_void_p), ints.shape[0],
+                                         out.ctypes.data_as(C.c_void_p), N.TAE_MEM_HOST))
+        return out
+
     def synchronize(self):
         check(lib().tae_synchronize(self._h))
 
@@ -193,7 +211,8 @@ class ClientKey:
         self.param_set = param_set
         self.context = context
         self.params = N.get_params(param_set)
-        self.lwe_size = self.params["k"] * self.params["N"] + 1
+        self.lwe_size = N.bit_len(param_set)
+        self.int_size = self.params["k"] * self.params["N"] + 1
 
     def __del__(self):
         try:
@@ -223,6 +242,21 @@ class ClientKey:
         cts = np.ascontiguousarray(cts, dtype=np.uint64).reshape(-1, self.lwe_size)
         out = np.zeros(cts.shape[0], dtype=np.uint8)
         check(lib().tae_decrypt_bits_raw(self._h, cts.ctypes.data_as(C.c_void_p), cts.shape[0],
+                                         out.ctypes.data_as(C.c_void_p)))
+        return out
+
+    # 8-bit model integers: shortint encrypt_without_padding / decrypt_without_padding
+    def encrypt_ints_raw(self, values, start_index: int) -> np.ndarray:
+        values = np.ascontiguousarray(np.asarray(values, dtype=np.uint8).ravel())
+        out = np.zeros((values.size, self.int_size), dtype=np.uint64)
+        check(lib().tae_encrypt_ints_raw(self._h, values.ctypes.data_as(C.c_void_p), values.size, start_index,
+                                         out.ctypes.data_as(C.c_void_p)))
+        return out
+
+    def decrypt_ints_raw(self, cts: np.ndarray) -> np.ndarray:
+        cts = np.ascontiguousarray(cts, dtype=np.uint64).reshape(-1, self.int_size)
+        out = np.zeros(cts.shape[0], dtype=np.uint8)
+        check(lib().tae_decrypt_ints_raw(self._h, cts.ctypes.data_as(C.c_void_p), cts.shape[0],
                                          out.ctypes.data_as(C.c_void_p)))
         return out
 
