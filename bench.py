@@ -31,7 +31,7 @@ README_KEY = bytes.fromhex("76b8e0ada0f13d90405d6ae55386bd28")  # README / main.
 README_IV = bytes.fromhex("bdd219b8a08ded1a")
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (= FP64 matrix) dense peak, spec
-PBS_KERNEL = "tae::br512x2::br_kernel<3, true>"
+PBS_KERNELS = {"1bit": "tae::br512x2::br_kernel<3, true, 12>", "8bit": "tae::pbs_kernel<1024>"}
 
 
 def pbs_algorithmic(p, bits):
@@ -58,7 +58,11 @@ def main():
     ap.add_argument("--key-schedule", choices=["fhe", "plain"], default="fhe")
     ap.add_argument("--cpu-baseline", choices=["auto", "on", "off"], default="auto")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--model", choices=["1bit", "8bit"], default="1bit",
+                    help="1bit: ShortintWoppbs1BitSboxGalMulPbsAesEncrypt (params_sqrd_lvl_64, the metric); "
+                         "8bit: ShortintWoppbs8BitSboxPbsAesEncrypt (BASELINE config #5)")
     args = ap.parse_args()
+    PBS_KERNEL = PBS_KERNELS[args.model]
 
     import torch  # plumbing: device memory + torch.distributed (nccl == RCCL)
     import tfhe_aes
@@ -75,9 +79,11 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
     threads = min(16, os.cpu_count() or 1)
-    pid = tfhe_aes.PARAMS_SQRD_LVL_64
+    pid = tfhe_aes.PARAMS_SQRD_LVL_64 if args.model == "1bit" else tfhe_aes.PARAMS_WOPPBS_8BIT
     p = tfhe_aes.get_params(pid)
-    L = p["k"] * p["N"] + 1
+    L = tfhe_aes.bit_len(pid)  # one bit ciphertext: big key (1-bit model) or small key (8-bit model)
+    E = (aes_128.ShortintWoppbs1BitSboxGalMulPbsAesEncrypt if args.model == "1bit"
+         else aes_128.ShortintWoppbs8BitSboxPbsAesEncrypt)
 
     # ---- keys: generated on rank 0 (client side), server keys broadcast once over RCCL ----
     t = time.time()
@@ -105,7 +111,7 @@ def main():
     if rank == 0:
         if args.key_schedule == "fhe":
             key_bits = aes_128.encrypt_byte_array(ck, README_KEY)
-            ek = aes_128.ShortintWoppbs1BitSboxGalMulPbsAesEncrypt.key_schedule(ctx, key_bits)
+            ek = E.key_schedule(ctx, key_bits)
             rk_np = np.stack([b.data(L) for w in ek for byte in w for b in byte])
             assert b"".join(aes_128.decrypt_byte_array(ck, w) for w in ek) == b"".join(
                 aes_128.key_schedule_plain(README_KEY)), "FHE key schedule mismatch"
@@ -130,7 +136,6 @@ def main():
     blk_dev = torch.from_numpy(cts.view(np.int64)).to(f"cuda:{dev}")
     out_dev = torch.empty_like(blk_dev)
     torch.cuda.synchronize()
-    E = aes_128.ShortintWoppbs1BitSboxGalMulPbsAesEncrypt
 
     def step():
         E.encrypt_blocks_device(ctx, rk_dev.data_ptr(), blk_dev.data_ptr(), nb, args.rounds, out_dev.data_ptr())
@@ -172,7 +177,7 @@ def main():
     ms_per_step = elapsed * 1000.0 / args.steps
 
     # ---- roofline of the dominant kernel (PBS = homomorphic_shift_boolean blind rotation) ----
-    launches = args.steps * args.rounds * p["cbs_l"]
+    launches = stage_ms.get("pbs_launches", 0)
     pbs_ms = stage_ms.get("pbs", 0.0) / max(launches, 1)
     bytes_launch, flop_launch = pbs_algorithmic(p, nb * 16 * 8)
     gbs = bytes_launch / (pbs_ms * 1e-3) / 1e9 if pbs_ms > 0 else None
@@ -197,19 +202,22 @@ def main():
                 "hbm": {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": (gbs / HBM_PEAK_GBS) if gbs else None,
                         "algorithmic_bytes_per_launch": bytes_launch}}
-    stage_share = {k: v / args.steps for k, v in stage_ms.items()}
+    stage_share = {k: v / args.steps for k, v in stage_ms.items() if k != "pbs_launches"}
 
     cpu = None
     want_cpu = args.cpu_baseline == "on" or (args.cpu_baseline == "auto" and world == 1)
     if want_cpu and rank == 0:
-        cpu = cpu_baseline(raw, ck, min(args.cpu_threads, os.cpu_count() or 1))
+        cpu = cpu_baseline(raw, ck, min(args.cpu_threads, os.cpu_count() or 1), args.model)
 
     if rank == 0:
         rec = {"metric": "FHE AES-128 blocks/sec", "value": value, "unit": "blocks/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-               "config": {"workload": f"{nb} counter-mode blocks per GPU, 10-round FHE AES-128 "
-                                      "(ShortintWoppbs1BitSboxGalMulPbsAesEncrypt, params_sqrd_lvl_64)",
+               "config": {"workload": f"{nb} counter-mode blocks per GPU, {args.rounds}-round FHE AES-128 ("
+                                      + ("ShortintWoppbs1BitSboxGalMulPbsAesEncrypt, params_sqrd_lvl_64)"
+                                         if args.model == "1bit" else
+                                         "ShortintWoppbs8BitSboxPbsAesEncrypt, shortint_woppbs_8bit params)"),
+                          "model": args.model,
                           "blocks_per_gpu": nb, "global_blocks": nb * world, "rounds": args.rounds,
                           "parallelism": f"blocks sharded over {world} GPU(s), keys broadcast once"},
                "roofline": roofline, "cpu_baseline": cpu,
@@ -221,24 +229,29 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(raw, ck, threads, min_s=10.0):
+def cpu_baseline(raw, ck, threads, model="1bit", min_s=10.0):
     """CPU oracle (restatement, kind "port") on a bounded sample of the same workload: the 16 SBOX
     circuit bootstraps of one AES round of one block, threads over bytes as the reference's rayon
-    (fhe_sbox_gal_mul_pbs.rs:33-41); blocks/s = 1 / (10 x round time)."""
+    (fhe_sbox_gal_mul_pbs.rs:33-41, fhe_sbox_pbs.rs:23-31); blocks/s = 1 / (10 x round time)."""
     from oracle import oracle
     from tfhe_aes import aes_128
-    ok = oracle.Keys(oracle.PARAMS_SQRD_LVL_64, None, raw=raw)
+    ok = oracle.Keys(oracle.PARAMS_SQRD_LVL_64 if model == "1bit" else oracle.PARAMS_WOPPBS_8BIT, None, raw=raw)
     blk = README_IV + (1).to_bytes(8, "big")
     cts = ck.encrypt_bits_raw(aes_128.blocks_to_bits([blk]), start_index=7 << 40)
     reps, t = 0, time.time()
     while True:  # bounded sample: whole rounds of 16 SBOX until >= min_s of CPU work
-        ok.sub_bytes_gal_mul(cts, threads)
+        if model == "1bit":
+            ok.sub_bytes_gal_mul(cts, threads)
+        else:
+            ok.sub_bytes8(cts, threads)
         reps += 1
         dt = time.time() - t
         if dt >= min_s:
             break
     return {"value": reps / (10 * dt), "unit": "blocks/s", "cores": threads, "kind": "port",
-            "sample": f"{reps} x 16 SBOX 8->24 circuit bootstraps (one AES round of one block each) on "
+            "sample": f"{reps} x 16 SBOX " + ("8->24 circuit bootstraps" if model == "1bit" else
+                                              "bootstrap_with_lut (CBS-VP + extract_bits)")
+                      + " (one AES round of one block each) on "
                       f"{threads} threads in {dt:.2f} s; blocks/s = rounds/s / 10"}
 
 

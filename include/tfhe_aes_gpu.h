@@ -174,6 +174,8 @@ int tae_synchronize(const tae_context *ctx);
 int tae_set_timing(const tae_context *ctx, int on);
 /* per-stage ms of the last batched call: [keyswitch, pbs, pfks, ggsw_fft, vp] */
 int tae_last_stage_times(const tae_context *ctx, float *ms5);
+/* [keyswitch, pbs, pfks, ggsw_fft, vp, extract_bits, linear] ms + the CBS-level PBS launch count */
+int tae_last_stage_times_v2(const tae_context *ctx, float *ms8);
 
 #ifdef __cplusplus
 }

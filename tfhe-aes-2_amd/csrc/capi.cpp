@@ -541,6 +541,16 @@ int tae_set_timing(const tae_context *ctx, int on) {
     });
 }
 
+int tae_last_stage_times_v2(const tae_context *ctx, float *ms8) {
+    return guarded([&] {
+        require(ctx && ms8, "null");
+        const auto &t = ctx->ctx->engine().last_times();
+        const float v[8] = {t.keyswitch, t.pbs, t.pfks, t.ggsw_fft, t.vertical_packing, t.extract, t.linear,
+                            (float)t.pbs_launches};
+        for (int i = 0; i < 8; i++) ms8[i] = v[i];
+    });
+}
+
 int tae_last_stage_times(const tae_context *ctx, float *ms5) {
     return guarded([&] {
         require(ctx && ms5, "null");

@@ -27,9 +27,10 @@ void hip_check(hipError_t e, const char *what);
 
 // Timing of the most recent batched call, per stage (ms, HIP events on the engine stream).
 struct StageTimes {
-    float keyswitch = 0, pbs = 0, pfks = 0, ggsw_fft = 0, vertical_packing = 0, linear = 0;
-    int pbs_launches = 0;
+    float keyswitch = 0, pbs = 0, pfks = 0, ggsw_fft = 0, vertical_packing = 0, extract = 0, linear = 0;
+    int pbs_launches = 0;  // CBS-level PBS launches (one homomorphic_shift_boolean batch each)
 };
+enum Stage { ST_KS = 0, ST_PBS, ST_PFKS, ST_FFT, ST_VP, ST_EXTRACT, ST_LINEAR };
 
 class Engine {
   public:
@@ -132,7 +133,18 @@ class Engine {
              *d_muls_ = nullptr;
     cplx *d_ggsw_f_ = nullptr;
     size_t cap_small_ = 0, cap_big_ = 0, cap_ggsw_ = 0, cap_ggsw_f_ = 0, cap_state_ = 0, cap_muls_ = 0;
-    hipEvent_t ev_[8];
+    // stage timing (HIP events around each stage call on the engine stream, summed in collect_times)
+    struct Span {
+        hipEvent_t a, b;
+        int stage;
+    };
+    std::vector<hipEvent_t> ev_pool_;
+    size_t ev_used_ = 0;
+    std::vector<Span> spans_;
+    hipEvent_t next_event();
+    template <class F>
+    void timed(int stage, F fn);
+    void collect_times();
     // int8 MFMA keyswitches (ksgemm.hpp): key limb matrices + digit scratch
     bool mfma_ks_ = false;
     int8_t *d_pf_bt_ = nullptr, *d_ks_bt_ = nullptr, *d_digits_ = nullptr;

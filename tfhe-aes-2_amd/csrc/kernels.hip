@@ -511,7 +511,6 @@ T *Engine::grow(T *&ptr, size_t &cap, size_t count) {
 void Engine::init_common() {
     HIPC(hipSetDevice(device_));
     HIPC(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-    for (auto &e : ev_) HIPC(hipEventCreate(&e));
     if (p_.N != 512 && p_.N != 1024) throw std::runtime_error("unsupported polynomial size");
     const FftTables t = make_fft_tables(p_.N);
     const size_t tb = sizeof(double) * 2 * t.M;
@@ -688,7 +687,7 @@ Engine::~Engine() {
                     (void *)d_digits_, (void *)d_wlut_sbox_, (void *)d_wlut_id_, (void *)d_lut_x_, (void *)d_xbuf_,
                     (void *)d_xsh_, (void *)d_xks_, (void *)d_xpbs_, (void *)d_ints_})
         if (q) hipFree(q);
-    for (auto &e : ev_) hipEventDestroy(e);
+    for (auto &e : ev_pool_) hipEventDestroy(e);
     hipStreamDestroy(stream_);
 }
 
@@ -837,23 +836,53 @@ void Engine::vertical_packing(const cplx *d_ggsw_f, size_t G, int n_in, const ui
     }
 }
 
+hipEvent_t Engine::next_event() {
+    if (ev_used_ == ev_pool_.size()) {
+        hipEvent_t e;
+        HIPC(hipEventCreate(&e));
+        ev_pool_.push_back(e);
+    }
+    return ev_pool_[ev_used_++];
+}
+
+template <class F>
+void Engine::timed(int stage, F fn) {
+    if (!timing_) {
+        fn();
+        return;
+    }
+    Span sp{next_event(), next_event(), stage};
+    HIPC(hipEventRecord(sp.a, stream_));
+    fn();
+    HIPC(hipEventRecord(sp.b, stream_));
+    spans_.push_back(sp);
+}
+
+void Engine::collect_times() {
+    if (spans_.empty()) return;
+    HIPC(hipEventSynchronize(spans_.back().b));
+    for (const Span &sp : spans_) {
+        float ms = 0;
+        HIPC(hipEventElapsedTime(&ms, sp.a, sp.b));
+        float *dst[] = {&times_.keyswitch, &times_.pbs, &times_.pfks, &times_.ggsw_fft, &times_.vertical_packing,
+                        &times_.extract, &times_.linear};
+        *dst[sp.stage] += ms;
+    }
+    spans_.clear();
+    ev_used_ = 0;
+}
+
 void Engine::circuit_bootstrap(const uint64_t *d_bits, size_t G, int n_in, const uint64_t *d_lut, int n_out,
                                uint64_t *d_out) {
     const size_t bits = G * n_in;
     reserve(bits, G * n_out);
-    if (timing_) HIPC(hipEventRecord(ev_[0], stream_));
-    keyswitch(d_bits, d_small_, bits);
-    if (timing_) HIPC(hipEventRecord(ev_[1], stream_));
+    timed(ST_KS, [&] { keyswitch(d_bits, d_small_, bits); });
     cbs_vp_stages(d_small_, G, n_in, d_lut, n_out, d_out);
 }
 
 void Engine::cbs_vp(const uint64_t *d_small_bits, size_t G, int n_in, const uint64_t *d_lut, int n_out,
                     uint64_t *d_out) {
     reserve(G * n_in, G * n_out);
-    if (timing_) {
-        HIPC(hipEventRecord(ev_[0], stream_));
-        HIPC(hipEventRecord(ev_[1], stream_));
-    }
     cbs_vp_stages(d_small_bits, G, n_in, d_lut, n_out, d_out);
 }
 
@@ -863,25 +892,13 @@ void Engine::cbs_vp_stages(const uint64_t *d_small_bits, size_t G, int n_in, con
                            uint64_t *d_out) {
     const size_t bits = G * n_in;
     for (int lev = 1; lev <= p_.cbs_l; lev++) {
-        pbs_shift_boolean(d_small_bits, d_big_, bits, lev);
-        if (timing_ && lev == p_.cbs_l) HIPC(hipEventRecord(ev_[2], stream_));
-        pfks_into_ggsw(d_big_, d_ggsw_, bits, lev);
+        timed(ST_PBS, [&] { pbs_shift_boolean(d_small_bits, d_big_, bits, lev); });
+        if (timing_) times_.pbs_launches++;
+        timed(ST_PFKS, [&] { pfks_into_ggsw(d_big_, d_ggsw_, bits, lev); });
     }
-    if (timing_) HIPC(hipEventRecord(ev_[3], stream_));
-    ggsw_to_fourier(d_ggsw_, d_ggsw_f_, bits);
-    if (timing_) HIPC(hipEventRecord(ev_[4], stream_));
-    vertical_packing(d_ggsw_f_, G, n_in, d_lut, n_out, d_out);
-    if (timing_) {
-        HIPC(hipEventRecord(ev_[5], stream_));
-        HIPC(hipEventSynchronize(ev_[5]));
-        float ms;
-        HIPC(hipEventElapsedTime(&ms, ev_[0], ev_[1])); times_.keyswitch += ms;
-        HIPC(hipEventElapsedTime(&ms, ev_[1], ev_[2])); times_.pbs += ms;
-        HIPC(hipEventElapsedTime(&ms, ev_[2], ev_[3])); times_.pfks += ms;
-        HIPC(hipEventElapsedTime(&ms, ev_[3], ev_[4])); times_.ggsw_fft += ms;
-        HIPC(hipEventElapsedTime(&ms, ev_[4], ev_[5])); times_.vertical_packing += ms;
-        times_.pbs_launches += p_.cbs_l;
-    }
+    timed(ST_FFT, [&] { ggsw_to_fourier(d_ggsw_, d_ggsw_f_, bits); });
+    timed(ST_VP, [&] { vertical_packing(d_ggsw_f_, G, n_in, d_lut, n_out, d_out); });
+    collect_times();
 }
 
 void Engine::extract_bits(const uint64_t *d_in, size_t B, int delta_log, int nbits, uint64_t *d_out) {
@@ -929,7 +946,8 @@ void Engine::bootstrap_bytes8(const uint64_t *d_bytes, size_t G, const uint64_t 
     if (!G) return;
     grow(d_ints_, cap_ints_, G * p_.big_len());
     cbs_vp(d_bytes, G, 8, d_lut, 1, d_ints_);
-    extract_bits(d_ints_, G, 56, 8, d_out);
+    timed(ST_EXTRACT, [&] { extract_bits(d_ints_, G, 56, 8, d_out); });
+    collect_times();
 }
 
 void Engine::aes8_encrypt_blocks(const uint64_t *d_rk, const uint64_t *d_blocks, size_t nb, int rounds,

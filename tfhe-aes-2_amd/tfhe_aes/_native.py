@@ -30,6 +30,7 @@ EXPORTED = [
     "tae_stage_bootstrap", "tae_stage_pfks_ggsw", "tae_stage_ggsw_fourier", "tae_stage_vertical_packing",
     "tae_synchronize", "tae_set_timing", "tae_last_stage_times", "tae_bit_len", "tae_encrypt_ints_raw",
     "tae_decrypt_ints_raw", "tae_bootstrap_from_bits_raw", "tae_extract_bits_raw", "tae_aes_key_schedule_raw",
+    "tae_last_stage_times_v2",
 ]
 
 
@@ -117,6 +118,7 @@ def lib() -> C.CDLL:
         "tae_bootstrap_from_bits_raw": ([vp, vp, sz, vp, vp, C.c_int], C.c_int),
         "tae_extract_bits_raw": ([vp, vp, sz, vp, C.c_int], C.c_int),
         "tae_aes_key_schedule_raw": ([vp, vp, vp, C.c_int], C.c_int),
+        "tae_last_stage_times_v2": ([vp, C.POINTER(C.c_float)], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -198,9 +198,11 @@ class FheContext:
         check(lib().tae_set_timing(self._h, 1 if on else 0))
 
     def last_stage_times(self) -> dict:
-        arr = (C.c_float * 5)()
-        check(lib().tae_last_stage_times(self._h, arr))
-        return dict(zip(("keyswitch", "pbs", "pfks", "ggsw_fft", "vertical_packing"), list(arr)))
+        arr = (C.c_float * 8)()
+        check(lib().tae_last_stage_times_v2(self._h, arr))
+        d = dict(zip(("keyswitch", "pbs", "pfks", "ggsw_fft", "vertical_packing", "extract_bits", "linear"), list(arr)))
+        d["pbs_launches"] = int(arr[7])
+        return d
 
 
 class ClientKey:
