@@ -184,7 +184,7 @@ def main():
     tflops = flop_launch / (pbs_ms * 1e-3) / 1e12 if pbs_ms > 0 else None
     # HBM traffic per launch of the same kernel from the committed PMC pass (scripts/bench_profile.sh
     # -> scripts/prof_summary.py: 2 x FETCH_SIZE + WRITE_SIZE), valid only for the same batch shape.
-    traffic, traffic_src = None, None
+    traffic, traffic_src, traffic_dram = None, None, None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if os.path.exists(pmc_path):
         with open(pmc_path) as fh:
@@ -192,11 +192,12 @@ def main():
         ent = pm.get("kernels", {}).get(PBS_KERNEL, {})
         if pm.get("blocks_per_gpu") == nb and "hbm_bytes_per_launch" in ent:
             traffic, traffic_src = ent["hbm_bytes_per_launch"], pm.get("source")
+            traffic_dram = ent.get("hbm_dram_bytes_per_launch")
     # The batched blind rotation is FP64-bound (>= 10 flop/B at any batch); its roofline
     # is the chip's dense f64 peak (MFMA and VALU alike on MI355X), HBM figures ride along.
     roofline = {"bound": "mfma", "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": (tflops / FP64_PEAK_TFLOPS) if tflops else None, "traffic": traffic,
-                "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
+                "traffic_unit": "bytes/launch", "traffic_source": traffic_src, "traffic_dram": traffic_dram,
                 "kernel": PBS_KERNEL + " (homomorphic_shift_boolean blind rotation)", "avg_launch_ms": pbs_ms,
                 "algorithmic_flop_per_launch": flop_launch,
                 "hbm": {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -220,6 +220,11 @@ __global__ void __launch_bounds__(THREADS, 1)
 
     const int steps = PBS ? n : n_in;
     uint64_t a_next = (PBS && jvalid) ? lwe_in[(size_t)(ct0 + jct) * (n + 1)] : 0;
+#if defined(TAE_DBG_PRIO1)
+    if (half) __builtin_amdgcn_s_setprio(1);
+#elif defined(TAE_DBG_PRIO0)
+    if (!half) __builtin_amdgcn_s_setprio(1);
+#endif
     cplx accr[8];
     cplx gv[K1 * 3];
     for (int step = 0; step < steps; step++) {

@@ -1,0 +1,338 @@
+// Batched blind rotation for N = 512, k = 4 with FOUR waves per SIMD: 1024-thread workgroups.
+//
+// Same work split as br512x2.hpp (C = 3 ciphertexts per workgroup, ACC and one level of spectra in
+// LDS, GGSW values shared by the three accumulators of a Fourier position), but every FFT job
+// (ciphertext, polynomial) is one whole wave: lane (u, r) = (lane & 15, lane >> 4) holds the four
+// points x[r + 4 i] of column (or row) u of the 16 x 16 FFT.  A DFT16 then runs as
+//   DFT4 over i in registers -> W16^{r k1} -> 4 x 4 transpose across the lanes u, u+16, u+32, u+48
+//   (two v_permlane32_swap and two v_permlane16_swap per complex pair, semantics probed by
+//   scripts/probes/permlane_swap.hip) -> DFT4 over r,
+// every output getting the oracle's DFT16 operation sequence (tfhe_oracle.c); the W16^0 / W16^4
+// factors are generic products with exact (1, 0) / (0, -1) and change nothing but signs of zeros.
+// 16 waves (15 jobs + 1 idle) give the SIMDs four waves each to hide LDS, GGSW-load and f64
+// latencies; registers are held under 128 per lane.  The MAC splits the 15 (q, ct) accumulators of
+// a Fourier position 4/4/4/3 over four 256-thread groups (one wave of each group per SIMD).
+// Lane (u, r) of a job decomposes and updates the ACC coefficients j = u + 16 r + 64 i (+ 256), so
+// each LDS access of a wave touches 64 consecutive coefficients.
+#pragma once
+#include "br512.hpp"
+#include "br512x2.hpp"
+
+namespace tae {
+namespace br512x4 {
+
+using br512::BUF_STRIDE;
+using br512::K1;
+using br512::lds_sync;
+using br512::M;
+using br512::N;
+using br512::pidx;
+using br512::u32x4;
+using br512::W16;
+using br512x2::mac_pos;
+using br512x2::swap16;
+using br512x2::wave_sync;
+
+constexpr int C = 3, JOBS = C * K1, THREADS = 1024;
+constexpr int ACC_STRIDE = N;
+
+__device__ __forceinline__ void swap32(cplx &x, cplx &y) {
+    // v_permlane32_swap: lanes 0-31 keep x and receive the partner's (lane + 32) x in y; lanes 32-63
+    // receive the partner's y in x and keep y
+    u32x4 a, b;
+    __builtin_memcpy(&a, &x, 16);
+    __builtin_memcpy(&b, &y, 16);
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        const auto r = __builtin_amdgcn_permlane32_swap(a[w], b[w], false, false);
+        a[w] = r[0];
+        b[w] = r[1];
+    }
+    __builtin_memcpy(&x, &a, 16);
+    __builtin_memcpy(&y, &b, 16);
+}
+
+// DFT16 over the lanes (u, 0..3) of a row group: in v[i] = x[r + 4 i], out v[k2] = X[r + 4 k2];
+// tw[k1 - 1] = W16^{r k1} (forward values).  Stage-1 outputs M[r][k1] are transposed to
+// M[0..3][r]: swap32 on k1 bit 1 vs r bit 1, then swap16 on bit 0.
+template <bool INV>
+__device__ __forceinline__ void dft16x4(cplx *v, const cplx *tw) {
+    dft4<INV>(v[0], v[1], v[2], v[3]);
+    v[1] = cmul(v[1], INV ? cconj(tw[0]) : tw[0]);
+    v[2] = cmul(v[2], INV ? cconj(tw[1]) : tw[1]);
+    v[3] = cmul(v[3], INV ? cconj(tw[2]) : tw[2]);
+    swap32(v[0], v[2]);
+    swap32(v[1], v[3]);
+    swap16(v[0], v[1]);
+    swap16(v[2], v[3]);
+    dft4<INV>(v[0], v[1], v[2], v[3]);
+}
+
+// MAC of one level for group G (accumulators pi = 4G .. min(4G+4, 15), (q, ct) = (pi / 3, pi % 3));
+// gv[p * 2 + (q - Q0)], per accumulator p ascending with the oracle's fma chain.
+template <int G>
+__device__ __forceinline__ void mac_level(const cplx *buf, int pos, cplx *accr, const cplx *gv) {
+    constexpr int PI0 = 4 * G, NA = (15 - PI0) < 4 ? (15 - PI0) : 4, Q0 = PI0 / 3;
+#pragma unroll
+    for (int p = 0; p < K1; p++) {
+        cplx x[C];
+#pragma unroll
+        for (int c = 0; c < C; c++) x[c] = buf[(c * K1 + p) * BUF_STRIDE + pos];
+#pragma unroll
+        for (int a = 0; a < NA; a++) {
+            const int pi = PI0 + a, q = pi / 3, c = pi % 3;
+            const cplx gg = gv[p * 2 + (q - Q0)];
+            double re = accr[a].re, im = accr[a].im;
+            re = fma(x[c].re, gg.re, re);
+            re = fma(-x[c].im, gg.im, re);
+            im = fma(x[c].re, gg.im, im);
+            im = fma(x[c].im, gg.re, im);
+            accr[a] = {re, im};
+        }
+    }
+}
+
+template <int G>
+__device__ __forceinline__ void mac_store(cplx *buf, int pos, const cplx *accr) {
+    constexpr int PI0 = 4 * G, NA = (15 - PI0) < 4 ? (15 - PI0) : 4;
+#pragma unroll
+    for (int a = 0; a < NA; a++) {
+        const int pi = PI0 + a, q = pi / 3, c = pi % 3;
+        buf[(c * K1 + q) * BUF_STRIDE + pos] = accr[a];
+    }
+}
+
+// Mode: PBS -> GGSW_i = bsk + i * ggsw_sz, per-ciphertext rotation a~_i; steps = n.
+//       VP  -> GGSW_t = ggsw_f + (g * n_in + b) * ggsw_sz, rotation X^{-2^t} shared; steps = n_in.
+template <int LEV, bool PBS, int BLOG>
+__global__ void __launch_bounds__(THREADS, 1)
+    br_kernel(const uint64_t *__restrict__ lwe_in, int n, const uint64_t *__restrict__ lut, int n_out,
+              const cplx *__restrict__ ggsw_base, int n_in, uint64_t *__restrict__ out, long B,
+              uint64_t body_add, uint64_t out_add, const cplx *__restrict__ twist, const cplx *__restrict__ wtab) {
+    constexpr int LOGN = 9;
+    extern __shared__ __align__(16) unsigned char smem[];
+    uint64_t *acc = reinterpret_cast<uint64_t *>(smem);             // [JOBS][ACC_STRIDE]
+    cplx *buf = reinterpret_cast<cplx *>(acc + JOBS * ACC_STRIDE);  // [JOBS][BUF_STRIDE]
+    cplx *s_tw = buf + JOBS * BUF_STRIDE;                           // twist e^{i pi j / N}
+    cplx *s_twa = s_tw + M;                                         // [16 a + b] = W_M^{a b}
+    cplx *s_utw = s_twa + M;                                        // conj(twist) 2^-8 (exact)
+    cplx *s_w16 = s_utw + M;                                        // [r][3]: W16^{r k1}, k1 = 1..3
+    const int tid = threadIdx.x;
+    const int jb = __builtin_amdgcn_readfirstlane(tid >> 6);  // job = wave
+    const int lane = tid & 63, u = lane & 15, r = lane >> 4;
+    const bool fjob = jb < JOBS;
+    const int jct = fjob ? jb / K1 : 0;
+    const size_t ggsw_sz = (size_t)LEV * K1 * K1 * M;
+
+    long ct0, g = 0;
+    int nct;
+    if (PBS) {
+        ct0 = (long)blockIdx.x * C;
+        nct = (int)min((long)C, B - ct0);
+    } else {
+        const int per_group = (n_out + C - 1) / C;
+        g = blockIdx.x / per_group;
+        ct0 = (long)(blockIdx.x - g * per_group) * C;
+        nct = min(C, n_out - (int)ct0);
+    }
+    const bool jvalid = fjob && jct < nct;
+
+    for (int t = tid; t < M; t += THREADS) {
+        s_tw[t] = twist[t];
+        s_twa[t] = wtab[(t >> 4) * (t & 15)];
+        s_utw[t] = cplx{twist[t].re * 0x1p-8, -twist[t].im * 0x1p-8};
+    }
+    if (tid < 12) {
+        // s_w16[3 r + k1 - 1] = W16^{r k1} = W_M^{16 e}, e = r k1 mod 16; exact 1 and -i for e = 0, 4
+        const int rr = tid / 3, k1 = tid - 3 * rr + 1;
+        const int e = (rr * k1) & 15;
+        const cplx w = wtab[16 * e];
+        s_w16[tid] = e == 0 ? cplx{1.0, 0.0} : (e == 4 ? cplx{0.0, -1.0} : w);
+    }
+
+    const cplx *gbase = PBS ? ggsw_base : ggsw_base + (size_t)g * n_in * ggsw_sz;
+    const uint32_t gbytes = (uint32_t)((size_t)(PBS ? n : n_in) * ggsw_sz * sizeof(cplx));
+    const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc((void *)gbase, (short)0, gbytes, 0x00020000);
+    const int grp = jb >> 2;  // MAC group (wave-uniform)
+    const int pos = mac_pos(tid & (M - 1));
+    const int gvoff = pos * (int)sizeof(cplx);
+    const int q0 = (4 * grp) / 3;           // first GGSW column of the group
+    const int nq = grp == 3 ? 1 : 2;        // columns it needs
+
+    for (int t = tid; t < JOBS * N; t += THREADS) {
+        const int job = t / N, j = t - job * N;
+        const int ct = job / K1, c = job - ct * K1;
+        uint64_t v = 0;
+        if (ct < nct) {
+            if (PBS) {
+                const uint64_t *in = lwe_in + (size_t)(ct0 + ct) * (n + 1);
+                const int bt = mod_switch(in[n] + body_add, LOGN);
+                const int e0 = (2 * N - (bt % (2 * N))) % (2 * N);
+                v = rotated_coeff(lut + c * N, j, e0, N);
+            } else {
+                v = c < K1 - 1 ? 0 : lut[(size_t)(ct0 + ct) * N + j];
+            }
+        }
+        acc[job * ACC_STRIDE + j] = v;
+    }
+    lds_sync();
+
+    const int steps = PBS ? n : n_in;
+    uint64_t a_next = (PBS && jvalid) ? lwe_in[(size_t)(ct0 + jct) * (n + 1)] : 0;
+    cplx accr[4];
+    cplx gv[K1 * 2];
+    const cplx *my_w16 = s_w16 + 3 * r;
+    for (int step = 0; step < steps; step++) {
+        int e, gstep;
+        if (PBS) {
+            const uint64_t a = a_next;
+            if (step + 1 < steps && jvalid) a_next = lwe_in[(size_t)(ct0 + jct) * (n + 1) + step + 1];
+            e = mod_switch(a, LOGN) % (2 * N);
+            gstep = step * (int)(ggsw_sz * sizeof(cplx));
+        } else {
+            const int b = n_in - 1 - step;
+            e = 2 * N - (1 << step);
+            gstep = b * (int)(ggsw_sz * sizeof(cplx));
+        }
+        // GGSW values (lev, p, q) at this thread's Fourier position, q in this group's columns
+        auto load_level = [&](int lev) {
+#pragma unroll
+            for (int p = 0; p < K1; p++)
+#pragma unroll
+                for (int qq = 0; qq < 2; qq++) {
+                    if (qq < nq) {
+                        const int soff = gstep + (((lev - 1) * K1 + p) * K1 + q0 + qq) * M * (int)sizeof(cplx);
+                        const u32x4 rv = __builtin_amdgcn_raw_buffer_load_b128(grs, gvoff, soff, 0);
+                        __builtin_memcpy(&gv[p * 2 + qq], &rv, sizeof(cplx));
+                    }
+                }
+        };
+        // ---- rotated difference + decomposition of coefficients j = u + 16 r + 64 i (+ M) ----
+        int ll = lane;
+        asm volatile("" : "+v"(ll));
+        uint32_t dig[LEV][4];
+        if (fjob) {
+            const uint64_t *poly = acc + jb * ACC_STRIDE;
+            // coefficient j of ACC * X^e is entry t = (j - e) mod 2N of [ACC, -ACC]
+            const int bt = ll - e;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int j = ll + 64 * i;
+                const int t = (bt + 64 * i) & (2 * N - 1);
+                const int ph = t & (N - 1);
+                const uint64_t m0 = (uint64_t)(int64_t)((t << 22) >> 31);
+                const uint64_t m1 = (uint64_t)(int64_t)(((t + M) << 22) >> 31);
+                const uint64_t v0 = poly[ph], v1 = poly[ph ^ M];
+                const uint64_t p0 = poly[j], p1 = poly[j + M];
+                const uint64_t x0 = (v0 ^ m0) - (p0 + m0), x1 = (v1 ^ m1) - (p1 + m1);
+                uint32_t d0[LEV], d1[LEV];
+                decompose16<LEV>(x0, BLOG, d0);
+                decompose16<LEV>(x1, BLOG, d1);
+#pragma unroll
+                for (int l = 0; l < LEV; l++) dig[l][i] = d0[l] | (d1[l] << 16);
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < 4; a++) accr[a] = cplx{0.0, 0.0};
+
+#pragma unroll
+        for (int lev = LEV; lev >= 1; lev--) {
+            load_level(lev);
+            // pass A (column u): twist, DFT16 over m = r + 4 i, W_M^{u k} -> LDS position u + 16 k
+            if (fjob) {
+                cplx v[4];
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    uint32_t dw = dig[0][i];
+#pragma unroll
+                    for (int l = 1; l < LEV; l++)
+                        if (lev - 1 == l) dw = dig[l][i];
+                    const double a0 = br512::lo16(dw), a1 = br512::hi16(dw);
+                    const cplx tw = s_tw[ll + 64 * i];
+                    v[i] = {fma(a0, tw.re, -(a1 * tw.im)), fma(a0, tw.im, a1 * tw.re)};
+                }
+                dft16x4<false>(v, my_w16);
+                cplx *dst = buf + jb * BUF_STRIDE;
+#pragma unroll
+                for (int k2 = 0; k2 < 4; k2++) {
+                    const int k = r + 4 * k2;
+                    dst[pidx(u + 16 * k)] = cmul(v[k2], s_twa[16 * k + u]);
+                }
+            }
+            wave_sync();
+            // pass B (row u): DFT16 over positions 16 u + r + 4 i, in place
+            if (fjob) {
+                cplx *base = buf + jb * BUF_STRIDE;
+                cplx v[4];
+#pragma unroll
+                for (int i = 0; i < 4; i++) v[i] = base[pidx(16 * u + r + 4 * i)];
+                dft16x4<false>(v, my_w16);
+#pragma unroll
+                for (int k2 = 0; k2 < 4; k2++) base[pidx(16 * u + r + 4 * k2)] = v[k2];
+            }
+            lds_sync();
+            switch (grp) {
+            case 0: mac_level<0>(buf, pidx(pos), accr, gv); break;
+            case 1: mac_level<1>(buf, pidx(pos), accr, gv); break;
+            case 2: mac_level<2>(buf, pidx(pos), accr, gv); break;
+            default: mac_level<3>(buf, pidx(pos), accr, gv); break;
+            }
+            lds_sync();
+        }
+        // ---- inverse FFT of the MAC results, accumulated into ACC ----
+        switch (grp) {
+        case 0: mac_store<0>(buf, pidx(pos), accr); break;
+        case 1: mac_store<1>(buf, pidx(pos), accr); break;
+        case 2: mac_store<2>(buf, pidx(pos), accr); break;
+        default: mac_store<3>(buf, pidx(pos), accr); break;
+        }
+        lds_sync();
+        if (fjob) {  // pass B^-1 (row u)
+            cplx *base = buf + jb * BUF_STRIDE;
+            cplx v[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) v[i] = base[pidx(16 * u + r + 4 * i)];
+            dft16x4<true>(v, my_w16);
+#pragma unroll
+            for (int k2 = 0; k2 < 4; k2++) base[pidx(16 * u + r + 4 * k2)] = v[k2];
+        }
+        wave_sync();
+        if (fjob) {  // pass A^-1 (column u): conj(W_M^{u kk}), DFT16^-1 over kk, untwist, from_torus, ACC +=
+            const cplx *src = buf + jb * BUF_STRIDE;
+            cplx v[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int kk = r + 4 * i;
+                v[i] = cmul(src[pidx(u + 16 * kk)], cconj(s_twa[16 * kk + u]));
+            }
+            dft16x4<true>(v, my_w16);
+            uint64_t *poly = acc + jb * ACC_STRIDE;
+#pragma unroll
+            for (int k2 = 0; k2 < 4; k2++) {
+                const int j = ll + 64 * k2;  // m = r + 4 k2 -> j = u + 16 m
+                const cplx t = cmul(v[k2], s_utw[j]);
+                poly[j] += from_torus_bits(t.re);
+                poly[j + M] += from_torus_bits(t.im);
+            }
+        }
+        wave_sync();
+    }
+    lds_sync();  // sample extraction reads every job's ACC
+    for (int ct = 0; ct < nct; ct++) {
+        const uint64_t *a = acc + ct * K1 * ACC_STRIDE;
+        uint64_t *o = PBS ? out + (size_t)(ct0 + ct) * (K1 - 1) * N + (size_t)(ct0 + ct)
+                          : out + ((size_t)g * n_out + ct0 + ct) * ((K1 - 1) * N + 1);
+        for (int t = tid; t < (K1 - 1) * N; t += THREADS) {
+            const int p = t / N, j = t - p * N;
+            o[t] = j == 0 ? a[p * ACC_STRIDE] : (0 - a[p * ACC_STRIDE + N - j]);
+        }
+        if (tid == 0) o[(K1 - 1) * N] = a[(K1 - 1) * ACC_STRIDE] + out_add;
+    }
+}
+
+inline size_t lds_bytes() {
+    return (size_t)JOBS * ACC_STRIDE * 8 + (size_t)JOBS * BUF_STRIDE * 16 + 3 * (size_t)M * 16 + 12 * 16;
+}
+
+}  // namespace br512x4
+}  // namespace tae

@@ -153,6 +153,7 @@ class Engine {
     void prepare_mfma_keys();
     double w16_[10] = {};     // W_16^{1,2,3,6,9} from the FFT table (batched N=512 kernels)
     bool batched512_ = false; // N == 512, k == 4: multi-ciphertext blind-rotation kernels
+    bool x4_512_ = false;     // ... as 1024-thread workgroups (br512x4.hpp; TAE_BR_X2=1 -> br512x2.hpp)
     bool wide512_ = false;    // ... as 512-thread workgroups (br512x2.hpp; TAE_BR_256=1 -> br512.hpp)
     bool timing_ = false;
     StageTimes times_;
