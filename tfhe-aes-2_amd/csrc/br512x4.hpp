@@ -226,8 +226,15 @@ __global__ void __launch_bounds__(THREADS, 1)
                 const uint64_t p0 = poly[j], p1 = poly[j + M];
                 const uint64_t x0 = (v0 ^ m0) - (p0 + m0), x1 = (v1 ^ m1) - (p1 + m1);
                 uint32_t d0[LEV], d1[LEV];
+#ifdef TAE_DBG_NODEC
+                for (int l = 0; l < LEV; l++) {
+                    d0[l] = (uint32_t)x0 & 0x7ff;
+                    d1[l] = (uint32_t)x1 & 0x7ff;
+                }
+#else
                 decompose16<LEV>(x0, BLOG, d0);
                 decompose16<LEV>(x1, BLOG, d1);
+#endif
 #pragma unroll
                 for (int l = 0; l < LEV; l++) dig[l][i] = d0[l] | (d1[l] << 16);
             }
@@ -237,7 +244,11 @@ __global__ void __launch_bounds__(THREADS, 1)
 
 #pragma unroll
         for (int lev = LEV; lev >= 1; lev--) {
+#ifndef TAE_DBG_NOGLOAD
             load_level(lev);
+#else
+            if (lev == LEV) load_level(lev);
+#endif
             // pass A (column u): twist, DFT16 over m = r + 4 i, W_M^{u k} -> LDS position u + 16 k
             if (fjob) {
                 cplx v[4];
@@ -270,14 +281,16 @@ __global__ void __launch_bounds__(THREADS, 1)
 #pragma unroll
                 for (int k2 = 0; k2 < 4; k2++) base[pidx(16 * u + r + 4 * k2)] = v[k2];
             }
-            lds_sync();
+            DBG_SYNC();
+#ifndef TAE_DBG_NOMAC
             switch (grp) {
             case 0: mac_level<0>(buf, pidx(pos), accr, gv); break;
             case 1: mac_level<1>(buf, pidx(pos), accr, gv); break;
             case 2: mac_level<2>(buf, pidx(pos), accr, gv); break;
             default: mac_level<3>(buf, pidx(pos), accr, gv); break;
             }
-            lds_sync();
+#endif
+            DBG_SYNC();
         }
         // ---- inverse FFT of the MAC results, accumulated into ACC ----
         switch (grp) {
@@ -286,7 +299,7 @@ __global__ void __launch_bounds__(THREADS, 1)
         case 2: mac_store<2>(buf, pidx(pos), accr); break;
         default: mac_store<3>(buf, pidx(pos), accr); break;
         }
-        lds_sync();
+        DBG_SYNC();
         if (fjob) {  // pass B^-1 (row u)
             cplx *base = buf + jb * BUF_STRIDE;
             cplx v[4];
@@ -311,8 +324,13 @@ __global__ void __launch_bounds__(THREADS, 1)
             for (int k2 = 0; k2 < 4; k2++) {
                 const int j = ll + 64 * k2;  // m = r + 4 k2 -> j = u + 16 m
                 const cplx t = cmul(v[k2], s_utw[j]);
+#ifdef TAE_DBG_NOTAIL
+                poly[j] += (uint64_t)__double_as_longlong(t.re);
+                poly[j + M] += (uint64_t)__double_as_longlong(t.im);
+#else
                 poly[j] += from_torus_bits(t.re);
                 poly[j + M] += from_torus_bits(t.im);
+#endif
             }
         }
         wave_sync();

@@ -638,6 +638,10 @@ Engine::Engine(const ServerKeyRaw &keys, int device) : p_(keys.p), device_(devic
 
 // Key limb matrices for the int8-MFMA keyswitches (ksgemm.hpp), built once on device.
 void Engine::prepare_mfma_keys() {
+    const char *bg = getenv("TAE_GEMM_SMALL");
+    big_gemm_ = !(bg && bg[0] == '1');
+    HIPC(hipFuncSetAttribute((const void *)ksgemm::gemm_big<4, 5>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)ksgemm::gemm_big_lds()));
     const char *v = getenv("TAE_KS_VALU");
     mfma_ks_ = !(v && v[0] == '1') && p_.pfks_b * 1 <= 16 && p_.ks_b <= 7;
     if (!mfma_ks_) return;
@@ -783,9 +787,18 @@ void Engine::pfks_into_ggsw(const uint64_t *d_big, uint64_t *d_ggsw, size_t B, i
         ksgemm::prep_digits<MA, LB><<<(unsigned)((thr + 255) / 256), 256, 0, stream_>>>(
             d_big, K + 1, d_digits_, (long)B, K + 1, kp_pf_, p_.pfks_b, p_.pfks_l);
         const int ncols = (p_.k + 1) * glwe;
+        const long out_stride = (long)p_.cbs_l * ncols;
+        if (big_gemm_) {
+            const long mtiles = (long)((B * MA + ksgemm::BTM - 1) / ksgemm::BTM);
+            const long ntiles = ((long)ncols * 8 + ksgemm::BTN - 1) / ksgemm::BTN;
+            ksgemm::gemm_big<MA, LB><<<(unsigned)(mtiles * ntiles), 512, ksgemm::gemm_big_lds(), stream_>>>(
+                d_digits_, d_pf_bt_, kp_pf_, (long)B * MA, mtiles, ncols, d_ggsw + (size_t)(level - 1) * ncols,
+                out_stride, (long)B, nullptr, 0, -1);
+            HIPC(hipGetLastError());
+            return;
+        }
         const long mtiles = (long)((B * MA + ksgemm::TM - 1) / ksgemm::TM);
         const long ntiles = ((long)ncols * 8 + ksgemm::TN - 1) / ksgemm::TN;
-        const long out_stride = (long)p_.cbs_l * ncols;
         ksgemm::gemm<MA, LB><<<(unsigned)(mtiles * ntiles), 256, 0, stream_>>>(
             d_digits_, d_pf_bt_, kp_pf_, (long)B * MA, mtiles, ncols, d_ggsw + (size_t)(level - 1) * ncols, out_stride,
             (long)B, nullptr, 0, -1);
