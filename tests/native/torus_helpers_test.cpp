@@ -22,6 +22,20 @@ static void check_ft(double x) {
     if (a != b && fails++ < 10) printf("from_torus(%a): got %016llx want %016llx\n", x, (unsigned long long)a, (unsigned long long)b);
 }
 
+template <int LEV, int B>
+static void check_dect(uint64_t x) {
+    uint32_t d[LEV];
+    int64_t r[LEV];
+    tae::decompose16t<LEV, B>(x, d);
+    or_decompose(x, B, LEV, r);
+    for (int l = 0; l < LEV; l++) {
+        const int64_t got = (int16_t)(d[l] & 0xFFFF);
+        if ((got != r[l] || (d[l] >> 16) != 0) && fails++ < 10)
+            printf("decompose16t(%016llx, B=%d, L=%d) level %d: got %lld want %lld\n", (unsigned long long)x, B, LEV,
+                   l + 1, (long long)got, (long long)r[l]);
+    }
+}
+
 template <int LEV>
 static void check_dec(uint64_t x, int B) {
     uint32_t d[LEV];
@@ -70,6 +84,10 @@ int main(int argc, char **argv) {
         check_dec<6>(x, 5);
         check_dec<4>(x, 6);
         check_dec<2>(x, 15);
+        check_dect<6, 7>(x);
+        check_dect<4, 6>(x);
+        check_dect<3, 12>(x);
+        check_dect<4, 9>(x);
     }
     for (long i = 0; i < n; i++) {
         uint64_t x = rng();
@@ -80,6 +98,10 @@ int main(int argc, char **argv) {
         check_dec<6>(x, 5);
         check_dec<4>(x, 6);
         check_dec<2>(x, 15);
+        check_dect<6, 7>(x);
+        check_dect<4, 6>(x);
+        check_dect<3, 12>(x);
+        check_dect<4, 9>(x);
     }
     printf("%s (%d mismatches)\n", fails ? "FAIL" : "OK", fails);
     return fails ? 1 : 0;

@@ -159,3 +159,25 @@ def test_aes8_full_fips197_with_fhe_key_schedule(gpu_context8, client8, golden):
     got = aes_128.bits_to_blocks(client8.decrypt_bits_raw(out))
     assert got[0].hex() == "69c4e0d86a7b0430d8cdb78070b4c55a"
     assert got == aes_128.expand_key_and_encrypt_blocks(key, blocks, 10)
+
+
+@pytest.mark.parametrize("pid", [tfhe_aes.PARAMS_SQRD_LVL_1, tfhe_aes.PARAMS_SQRD_LVL_256])
+def test_other_n1024_sets_bit_exact(pid, oracle_mod):
+    """The batched N=1024 blind rotation (br1024.hpp) under params_sqrd_lvl_1 (pbs 2 x 2^15) and _256
+    (pbs 4 x 2^9): homomorphic_shift_boolean and a 4 -> 4 circuit bootstrap, equal to the oracle."""
+    ck, keys = tfhe_aes.generate_keys_raw(pid, SEED, threads=THREADS)
+    ctx = tfhe_aes.context_from_raw(pid, keys, device=0)
+    ok = oracle_mod.Keys(pid, None, raw=keys)
+    p = tfhe_aes.get_params(pid)
+    big, small = p["k"] * p["N"] + 1, p["n"] + 1
+    cts = ck.encrypt_bits_raw([1, 0, 1, 1], start_index=90)
+    sm = np.stack([ok.keyswitch(c) for c in cts[:2]])
+    out = np.zeros((2, big), dtype=np.uint64)
+    _stage(N.lib().tae_stage_pbs_shift_boolean, ctx._h, _vp(sm), 2, 1, _vp(out), N.TAE_MEM_HOST)
+    for i in range(2):
+        assert np.array_equal(out[i], ok.homomorphic_shift_boolean(sm[i], 1)), i
+    f = lambda x: (x * 7 + 3) & 15
+    lut = ctx.generate_lookup_table(4, 4, f)
+    res = ctx.circuit_bootstrap_raw(cts.reshape(1, 4, big), lut)
+    assert np.array_equal(res[0], ok.circuit_bootstrap(cts, lut.as_array(), 4))
+    assert aes_128.bits_to_u8([0] * 4 + list(ck.decrypt_bits_raw(res[0]))) == f(0b1011)

@@ -1,0 +1,345 @@
+// Batched blind rotation for N = 1024, k = 2 (the 8-bit model's set, shortint_woppbs_8bit.rs:39-86,
+// and params_sqrd_lvl_1/4/256): C = 2 ciphertexts per 512-thread workgroup.
+//
+// Every FFT job (ciphertext, polynomial) is one wave: lane t runs the radix-8 DFT of each of the
+// three passes of the oracle's M = 512 schedule (FftPlan<512>: pass 0 on points t + 64 m, pass 1 on
+// 64 (t >> 3) + (t & 7) + 8 m, pass 2 on 8 t + m, twiddles w[u k], w[8 u k], none), exchanging
+// through the job's own LDS region (wave-local, no barrier).  The spectra live one decomposition
+// level at a time (pbs_l = 6); the MAC runs with thread = Fourier position (512) over the six
+// (q, ct) accumulators, each GGSW value loaded once for both ciphertexts.  Operation order per
+// output is the oracle's (explicit fma, the u k == 0 twiddles skipped as there), so results are
+// bit-exact.
+// LDS (126 KB): ACC [C][k+1][N] u64, spectra [C (k+1)][576] cplx (+1 pad per 8: conflict-free
+// b128 accesses at strides 1, 8 and 64), twist / W_512 / untwist tables.
+#pragma once
+#include "br512.hpp"
+
+namespace tae {
+namespace br1024 {
+
+constexpr int N = 1024, M = 512, K1 = 3, C = 2, JOBS = C * K1, THREADS = 512;
+
+// a job's lanes are one wave and a wave's LDS operations execute in order: hand-offs inside a job
+// only need the compiler not to reorder
+__device__ __forceinline__ void wave_sync() { asm volatile("" ::: "memory"); }
+constexpr int BUF_STRIDE = M + M / 8;  // cplx
+constexpr int ACC_STRIDE = N;          // u64
+
+__device__ __forceinline__ int pidx(int q) { return q + (q >> 3); }
+
+// c ? a : b on the two doubles (a struct select here went through scratch memory)
+__device__ __forceinline__ cplx csel(bool c, cplx a, cplx b) { return {c ? a.re : b.re, c ? a.im : b.im}; }
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// dft<8, 512, INV> of fft_device.hpp with the W8 factors from the table (w[64] = W8^1, w[192] = W8^3)
+template <bool INV>
+__device__ __forceinline__ void dft8(cplx *v, cplx w1, cplx w3) {
+    cplx y[8];
+#pragma unroll
+    for (int n1 = 0; n1 < 2; n1++) dft4<INV>(v[n1], v[n1 + 2], v[n1 + 4], v[n1 + 6]);
+#pragma unroll
+    for (int k1 = 0; k1 < 4; k1++) y[2 * k1] = v[2 * k1];
+    y[1] = v[1];
+    y[3] = cmul(v[3], INV ? cconj(w1) : w1);
+    y[5] = INV ? cplx{-v[5].im, v[5].re} : cplx{v[5].im, -v[5].re};
+    y[7] = cmul(v[7], INV ? cconj(w3) : w3);
+#pragma unroll
+    for (int k1 = 0; k1 < 4; k1++) {
+        const cplx a = y[2 * k1], b = y[2 * k1 + 1];
+        v[k1] = cadd(a, b);
+        v[k1 + 4] = csub(a, b);
+    }
+}
+
+// Mode: PBS -> GGSW_i = bsk + i * ggsw_sz, per-ciphertext rotation a~_i; steps = n.
+//       VP  -> GGSW_t = ggsw_f + (g * n_in + b) * ggsw_sz, rotation X^{-2^t} shared; steps = n_in.
+template <int LEV, bool PBS, int BLOG>
+__global__ void __launch_bounds__(THREADS, 1)
+    br_kernel(const uint64_t *__restrict__ lwe_in, int n, const uint64_t *__restrict__ lut, int n_out,
+              const cplx *__restrict__ ggsw_base, int n_in, uint64_t *__restrict__ out, long B,
+              uint64_t body_add, uint64_t out_add, const cplx *__restrict__ twist, const cplx *__restrict__ untwist,
+              const cplx *__restrict__ wtab) {
+    constexpr int LOGN = 10;
+    extern __shared__ __align__(16) unsigned char smem[];
+    uint64_t *acc = reinterpret_cast<uint64_t *>(smem);             // [JOBS][ACC_STRIDE]
+    cplx *buf = reinterpret_cast<cplx *>(acc + JOBS * ACC_STRIDE);  // [JOBS][BUF_STRIDE]
+    cplx *s_tw = buf + JOBS * BUF_STRIDE;                           // twist
+    cplx *s_w = s_tw + M;                                           // W_512 table
+    cplx *s_utw = s_w + M;                                          // untwist = conj(twist) / M
+    const int tid = threadIdx.x;
+    const int jb = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int t = tid & 63;
+    const bool fjob = jb < JOBS;
+    const int jct = fjob ? jb / K1 : 0;
+    const size_t ggsw_sz = (size_t)LEV * K1 * K1 * M;
+
+    long ct0, g = 0;
+    int nct;
+    if (PBS) {
+        ct0 = (long)blockIdx.x * C;
+        nct = (int)min((long)C, B - ct0);
+    } else {
+        const int per_group = (n_out + C - 1) / C;
+        g = blockIdx.x / per_group;
+        ct0 = (long)(blockIdx.x - g * per_group) * C;
+        nct = min(C, n_out - (int)ct0);
+    }
+    const bool jvalid = fjob && jct < nct;
+
+    for (int i = tid; i < M; i += THREADS) {
+        s_tw[i] = twist[i];
+        s_w[i] = wtab[i];
+        s_utw[i] = untwist[i];
+    }
+    const cplx *gbase = PBS ? ggsw_base : ggsw_base + (size_t)g * n_in * ggsw_sz;
+    const uint32_t gbytes = (uint32_t)((size_t)(PBS ? n : n_in) * ggsw_sz * sizeof(cplx));
+    const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc((void *)gbase, (short)0, gbytes, 0x00020000);
+    const int pos = tid;  // MAC: Fourier position
+    const int gvoff = pos * (int)sizeof(cplx);
+
+    for (int i = tid; i < JOBS * N; i += THREADS) {
+        const int job = i / N, j = i - job * N;
+        const int ct = job / K1, c = job - ct * K1;
+        uint64_t v = 0;
+        if (ct < nct) {
+            if (PBS) {
+                const uint64_t *in = lwe_in + (size_t)(ct0 + ct) * (n + 1);
+                const int bt = mod_switch(in[n] + body_add, LOGN);
+                const int e0 = (2 * N - (bt % (2 * N))) % (2 * N);
+                v = rotated_coeff(lut + c * N, j, e0, N);
+            } else {
+                v = c < K1 - 1 ? 0 : lut[(size_t)(ct0 + ct) * N + j];
+            }
+        }
+        acc[job * ACC_STRIDE + j] = v;
+    }
+    br512::lds_sync();
+    const cplx w81 = s_w[64], w83 = s_w[192];
+
+    const int steps = PBS ? n : n_in;
+    uint64_t a_next = (PBS && jvalid) ? lwe_in[(size_t)(ct0 + jct) * (n + 1)] : 0;
+    cplx accr[K1 * C];
+    cplx gv[K1 * K1];
+    for (int step = 0; step < steps; step++) {
+        int e, gstep;
+        if (PBS) {
+            const uint64_t a = a_next;
+            if (step + 1 < steps && jvalid) a_next = lwe_in[(size_t)(ct0 + jct) * (n + 1) + step + 1];
+            e = mod_switch(a, LOGN) % (2 * N);
+            gstep = step * (int)(ggsw_sz * sizeof(cplx));
+        } else {
+            const int b = n_in - 1 - step;
+            e = 2 * N - (1 << step);
+            gstep = b * (int)(ggsw_sz * sizeof(cplx));
+        }
+        // ---- rotated difference + decomposition of coefficients j = t + 64 m (+ M) ----
+        int tt = t;
+        asm volatile("" : "+v"(tt));
+        // digits: int16 pairs (x_j, x_{j+M}) per level, or for base_log <= 7 (the 8-bit model, up to 6
+        // levels) int8 quadruples holding two levels, so that the per-level loop needs no indexed array
+        constexpr bool BYTES = BLOG <= 7;
+        constexpr int DW = BYTES ? (LEV + 1) / 2 : LEV;
+        uint32_t dig[DW][8];
+        if (fjob) {
+            const uint64_t *poly = acc + jb * ACC_STRIDE;
+            const int bt = tt - e;
+#pragma unroll
+            for (int m = 0; m < 8; m++) {
+                const int j = tt + 64 * m;
+                const int ti = (bt + 64 * m) & (2 * N - 1);  // entry of [ACC, -ACC]
+                const int ph = ti & (N - 1);
+                const uint64_t m0 = (uint64_t)(int64_t)((ti << 21) >> 31);
+                const uint64_t m1 = (uint64_t)(int64_t)(((ti + M) << 21) >> 31);
+                const uint64_t v0 = poly[ph], v1 = poly[ph ^ M];
+                const uint64_t p0 = poly[j], p1 = poly[j + M];
+                const uint64_t x0 = (v0 ^ m0) - (p0 + m0), x1 = (v1 ^ m1) - (p1 + m1);
+                uint32_t d0[LEV], d1[LEV];
+                decompose16t<LEV, BLOG>(x0, d0);
+                decompose16t<LEV, BLOG>(x1, d1);
+                if constexpr (BYTES) {
+#pragma unroll
+                    for (int w = 0; w < DW; w++) {
+                        uint32_t v = (d0[2 * w] & 0xFF) | ((d1[2 * w] & 0xFF) << 8);
+                        if (2 * w + 1 < LEV) v |= ((d0[2 * w + 1] & 0xFF) << 16) | ((d1[2 * w + 1] & 0xFF) << 24);
+                        dig[w][m] = v;
+                    }
+                } else {
+#pragma unroll
+                    for (int l = 0; l < LEV; l++) dig[l][m] = d0[l] | (d1[l] << 16);
+                }
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < K1 * C; a++) accr[a] = cplx{0.0, 0.0};
+
+#pragma unroll(LEV <= 2 ? LEV : 1)
+        for (int lev = LEV; lev >= 1; lev--) {
+#pragma unroll
+            for (int p = 0; p < K1; p++)
+#pragma unroll
+                for (int q = 0; q < K1; q++) {
+                    const int soff = gstep + (((lev - 1) * K1 + p) * K1 + q) * M * (int)sizeof(cplx);
+                    const u32x4 rv = __builtin_amdgcn_raw_buffer_load_b128(grs, gvoff, soff, 0);
+                    __builtin_memcpy(&gv[p * K1 + q], &rv, sizeof(cplx));
+                }
+            if (fjob) {
+                cplx *X = buf + jb * BUF_STRIDE;
+                cplx v[8];
+                // pass 0: twist, DFT8 over m, w[t kk] -> position t + 64 kk
+#pragma unroll
+                for (int m = 0; m < 8; m++) {
+                    double a0, a1;
+                    if constexpr (BYTES) {
+                        const int wsel = (lev - 1) >> 1, sh = ((lev - 1) & 1) * 16;
+                        uint32_t dw = dig[0][m];
+#pragma unroll
+                        for (int w = 1; w < DW; w++) {  // mask select (a ternary became a scratch index)
+                            const uint32_t msk = 0u - (uint32_t)(wsel == w);
+                            dw = (dw & ~msk) | (dig[w][m] & msk);
+                        }
+                        a0 = (double)(int32_t)__builtin_amdgcn_sbfe(dw, sh, 8);
+                        a1 = (double)(int32_t)__builtin_amdgcn_sbfe(dw, sh + 8, 8);
+                    } else {
+                        uint32_t dw = dig[0][m];
+#pragma unroll
+                        for (int l = 1; l < LEV; l++) dw = lev - 1 == l ? dig[l][m] : dw;
+                        a0 = br512::lo16(dw);
+                        a1 = br512::hi16(dw);
+                    }
+                    const cplx tw = s_tw[tt + 64 * m];
+                    v[m] = {fma(a0, tw.re, -(a1 * tw.im)), fma(a0, tw.im, a1 * tw.re)};
+                }
+                dft8<false>(v, w81, w83);
+#pragma unroll
+                for (int kk = 0; kk < 8; kk++) {
+                    const cplx tv = cmul(v[kk], s_w[tt * kk]);
+                    X[pidx(tt + 64 * kk)] = csel(tt * kk != 0, tv, v[kk]);
+                }
+                wave_sync();
+                // pass 1: points 64 gg + uu + 8 m, w[8 uu kk]
+                {
+                    const int gg = tt >> 3, uu = tt & 7;
+#pragma unroll
+                    for (int m = 0; m < 8; m++) v[m] = X[pidx(64 * gg + uu + 8 * m)];
+                    dft8<false>(v, w81, w83);
+#pragma unroll
+                    for (int kk = 0; kk < 8; kk++) {
+                        const cplx tv = cmul(v[kk], s_w[8 * uu * kk]);
+                        X[pidx(64 * gg + uu + 8 * kk)] = csel(uu * kk != 0, tv, v[kk]);
+                    }
+                }
+                wave_sync();
+                // pass 2: points 8 t + m, no twiddles
+#pragma unroll
+                for (int m = 0; m < 8; m++) v[m] = X[pidx(8 * tt + m)];
+                dft8<false>(v, w81, w83);
+#pragma unroll
+                for (int kk = 0; kk < 8; kk++) X[pidx(8 * tt + kk)] = v[kk];
+            }
+            br512::lds_sync();
+            // MAC at Fourier position pos: accumulator (q, c) = accr[q * C + c], p ascending
+#pragma unroll
+            for (int p = 0; p < K1; p++) {
+                cplx x[C];
+#pragma unroll
+                for (int c = 0; c < C; c++) x[c] = buf[(c * K1 + p) * BUF_STRIDE + pidx(pos)];
+#pragma unroll
+                for (int q = 0; q < K1; q++)
+#pragma unroll
+                    for (int c = 0; c < C; c++) {
+                        const cplx gg = gv[p * K1 + q];
+                        double re = accr[q * C + c].re, im = accr[q * C + c].im;
+                        re = fma(x[c].re, gg.re, re);
+                        re = fma(-x[c].im, gg.im, re);
+                        im = fma(x[c].re, gg.im, im);
+                        im = fma(x[c].im, gg.re, im);
+                        accr[q * C + c] = {re, im};
+                    }
+            }
+            br512::lds_sync();
+        }
+        // ---- inverse FFT of the MAC results, accumulated into ACC ----
+#pragma unroll
+        for (int q = 0; q < K1; q++)
+#pragma unroll
+            for (int c = 0; c < C; c++) buf[(c * K1 + q) * BUF_STRIDE + pidx(pos)] = accr[q * C + c];
+        br512::lds_sync();
+        if (fjob) {
+            cplx *Y = buf + jb * BUF_STRIDE;
+            cplx v[8];
+            // inverse pass 2: points 8 t + kk, no twiddles
+#pragma unroll
+            for (int kk = 0; kk < 8; kk++) v[kk] = Y[pidx(8 * tt + kk)];
+            dft8<true>(v, w81, w83);
+#pragma unroll
+            for (int m = 0; m < 8; m++) Y[pidx(8 * tt + m)] = v[m];
+            wave_sync();
+            // inverse pass 1: conj(w[8 uu kk]) on points 64 gg + uu + 8 kk
+            {
+                const int gg = tt >> 3, uu = tt & 7;
+#pragma unroll
+                for (int kk = 0; kk < 8; kk++) {
+                    const cplx y = Y[pidx(64 * gg + uu + 8 * kk)];
+                    const cplx tv = cmul(y, cconj(s_w[8 * uu * kk]));
+                    v[kk] = csel(uu * kk != 0, tv, y);
+                }
+                dft8<true>(v, w81, w83);
+#pragma unroll
+                for (int m = 0; m < 8; m++) Y[pidx(64 * gg + uu + 8 * m)] = v[m];
+            }
+            wave_sync();
+            // inverse pass 0: conj(w[t kk]) on points t + 64 kk, untwist, from_torus, ACC +=
+#pragma unroll
+            for (int kk = 0; kk < 8; kk++) {
+                const cplx y = Y[pidx(tt + 64 * kk)];
+                const cplx tv = cmul(y, cconj(s_w[tt * kk]));
+                v[kk] = csel(tt * kk != 0, tv, y);
+            }
+            dft8<true>(v, w81, w83);
+            uint64_t *poly = acc + jb * ACC_STRIDE;
+#pragma unroll
+            for (int m = 0; m < 8; m++) {
+                const int j = tt + 64 * m;
+                const cplx r = cmul(v[m], s_utw[j]);
+                poly[j] += from_torus_bits(r.re);
+                poly[j + M] += from_torus_bits(r.im);
+            }
+        }
+        wave_sync();
+    }
+    br512::lds_sync();
+    for (int ct = 0; ct < nct; ct++) {
+        const uint64_t *a = acc + ct * K1 * ACC_STRIDE;
+        uint64_t *o = PBS ? out + (size_t)(ct0 + ct) * (K1 - 1) * N + (size_t)(ct0 + ct)
+                          : out + ((size_t)g * n_out + ct0 + ct) * ((K1 - 1) * N + 1);
+        for (int i = tid; i < (K1 - 1) * N; i += THREADS) {
+            const int p = i / N, j = i - p * N;
+            o[i] = j == 0 ? a[p * ACC_STRIDE] : (0 - a[p * ACC_STRIDE + N - j]);
+        }
+        if (tid == 0) o[(K1 - 1) * N] = a[(K1 - 1) * ACC_STRIDE] + out_add;
+    }
+}
+
+inline size_t lds_bytes() { return (size_t)JOBS * ACC_STRIDE * 8 + (size_t)JOBS * BUF_STRIDE * 16 + 3 * (size_t)M * 16; }
+
+// (levels, base_log) combinations of the N=1024 parameter sets: returns the kernel or nullptr
+typedef void (*kernel_t)(const uint64_t *, int, const uint64_t *, int, const cplx *, int, uint64_t *, long, uint64_t,
+                         uint64_t, const cplx *, const cplx *, const cplx *);
+inline kernel_t pick(bool pbs, int levels, int base_log) {
+#define TAE_BR1024(L, BL)                                                          \
+    if (levels == L && base_log == BL)                                             \
+        return pbs ? (kernel_t)br_kernel<L, true, BL> : (kernel_t)br_kernel<L, false, BL>;
+    TAE_BR1024(6, 7)   // 8-bit model PBS (shortint_woppbs_8bit.rs:39-86)
+    TAE_BR1024(4, 6)   // 8-bit model CBS GGSW
+    TAE_BR1024(2, 15)  // params_sqrd_lvl_1 / _4 PBS
+    TAE_BR1024(4, 9)   // params_sqrd_lvl_256 PBS
+    TAE_BR1024(1, 10)  // lvl_1 CBS
+    TAE_BR1024(1, 11)  // lvl_4 CBS
+    TAE_BR1024(1, 14)  // lvl_256 CBS
+#undef TAE_BR1024
+    return nullptr;
+}
+
+}  // namespace br1024
+}  // namespace tae

@@ -154,6 +154,10 @@ class Engine {
     void prepare_mfma_keys();
     double w16_[10] = {};     // W_16^{1,2,3,6,9} from the FFT table (batched N=512 kernels)
     bool batched512_ = false; // N == 512, k == 4: multi-ciphertext blind-rotation kernels
+    // batched N=1024, k=2 blind rotation (br1024.hpp) for this set's (levels, base_log), or nullptr
+    void (*br1024_pbs_)(const uint64_t *, int, const uint64_t *, int, const cplx *, int, uint64_t *, long, uint64_t,
+                        uint64_t, const cplx *, const cplx *, const cplx *) = nullptr;
+    decltype(br1024_pbs_) br1024_vp_ = nullptr;
     bool x4_512_ = false;     // ... as 1024-thread workgroups (br512x4.hpp; TAE_BR_X2=1 -> br512x2.hpp)
     bool wide512_ = false;    // ... as 512-thread workgroups (br512x2.hpp; TAE_BR_256=1 -> br512.hpp)
     bool timing_ = false;

@@ -181,6 +181,32 @@ __host__ __device__ __forceinline__ void decompose16(uint64_t x, int B, uint32_t
     }
 }
 
+// decompose16 for compile-time B (any LEV with B * LEV < 64): the state after the first level is
+// kept in 64 bits when B * (LEV - 1) >= 32 (the 8-bit model's PBS: 6 levels of 7 bits).
+template <int LEV, int B>
+__host__ __device__ __forceinline__ void decompose16t(uint64_t x, uint32_t *d) {
+    if constexpr (B * (LEV - 1) < 32) {
+        decompose16<LEV>(x, B, d);
+    } else {
+        constexpr int nrb = 64 - B * LEV;
+        const uint64_t X = x + (1ull << (nrb - 1));
+        constexpr uint64_t mask = (1ull << B) - 1;
+        constexpr uint32_t neg = 0x10000u - (1u << B);
+        uint64_t res = (X >> nrb) & mask;
+        uint64_t st = X >> (nrb + B);
+#pragma unroll
+        for (int l = LEV - 1; l >= 0; l--) {
+            const uint64_t c = (((res - 1) | st) & res) >> (B - 1);
+            d[l] = (uint32_t)res + (uint32_t)c * neg;
+            if (l > 0) {
+                st += c;
+                res = st & mask;
+                st >>= B;
+            }
+        }
+    }
+}
+
 // pbs_modulus_switch: round(x * 2N / 2^64) in [0, 2N]
 __device__ __forceinline__ int mod_switch(uint64_t x, int logN) {
     uint64_t o = x >> (64 - logN - 2);

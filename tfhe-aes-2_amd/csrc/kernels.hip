@@ -20,6 +20,7 @@
 #include "br512.hpp"
 #include "br512x2.hpp"
 #include "br512x4.hpp"
+#include "br1024.hpp"
 #include "ksgemm.hpp"
 #include "engine.hpp"
 #include "fft_device.hpp"
@@ -595,6 +596,15 @@ void Engine::init_common() {
         HIPC(hipFuncSetAttribute((const void *)br512::br_kernel<kBrC, 1, false>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     }
+    // batched N=1024, k=2 blind rotation (br1024.hpp); TAE_BR_V1=1 forces the one-ciphertext kernels
+    if (p_.N == 1024 && p_.k == 2 && !(v1 && v1[0] == '1')) {
+        br1024_pbs_ = br1024::pick(true, p_.pbs_l, p_.pbs_b);
+        br1024_vp_ = br1024::pick(false, p_.cbs_l, p_.cbs_b);
+        for (auto kf : {br1024_pbs_, br1024_vp_})
+            if (kf)
+                HIPC(hipFuncSetAttribute((const void *)kf, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)br1024::lds_bytes()));
+    }
     // opt-in to >64 KiB dynamic LDS for the blind-rotation kernels
     if (p_.N == 512) {
         HIPC(hipFuncSetAttribute((const void *)pbs_kernel<512>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -756,6 +766,13 @@ void Engine::bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint
         HIPC(hipGetLastError());
         return;
     }
+    if (br1024_pbs_) {
+        const size_t wgs = (B + br1024::C - 1) / br1024::C;
+        br1024_pbs_<<<(unsigned)wgs, br1024::THREADS, br1024::lds_bytes(), stream_>>>(
+            d_small, p_.n, d_lut_glwe, 0, d_bsk_f_, 0, d_big, (long)B, body_add, out_add, d_twist_, d_untwist_, d_w_);
+        HIPC(hipGetLastError());
+        return;
+    }
     for (size_t off = 0; off < B; off += 65535) {
         const unsigned g = (unsigned)std::min<size_t>(65535, B - off);
         if (p_.N == 512) {
@@ -850,6 +867,13 @@ void Engine::vertical_packing(const cplx *d_ggsw_f, size_t G, int n_in, const ui
         }
         br512::br_kernel<kBrC, 1, false><<<(unsigned)wgs, kThreads, br512::lds_bytes(kBrC), stream_>>>(
             nullptr, 0, d_lut, n_out, d_ggsw_f, n_in, d_out, (long)G, p_.cbs_b, 0, 0, d_twist_, d_w_, W);
+        HIPC(hipGetLastError());
+        return;
+    }
+    if (br1024_vp_) {
+        const size_t wgs = G * (size_t)((n_out + br1024::C - 1) / br1024::C);
+        br1024_vp_<<<(unsigned)wgs, br1024::THREADS, br1024::lds_bytes(), stream_>>>(
+            nullptr, 0, d_lut, n_out, d_ggsw_f, n_in, d_out, (long)G, 0, 0, d_twist_, d_untwist_, d_w_);
         HIPC(hipGetLastError());
         return;
     }
