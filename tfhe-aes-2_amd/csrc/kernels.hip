@@ -650,8 +650,12 @@ Engine::Engine(const ServerKeyRaw &keys, int device) : p_(keys.p), device_(devic
 void Engine::prepare_mfma_keys() {
     const char *bg = getenv("TAE_GEMM_SMALL");
     big_gemm_ = !(bg && bg[0] == '1');
+    const char *g4 = getenv("TAE_GEMM_MA4");
+    gemm3_ = !(g4 && g4[0] == '1');
     HIPC(hipFuncSetAttribute((const void *)ksgemm::gemm_big<4, 5>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)ksgemm::gemm_big_lds()));
+    HIPC(hipFuncSetAttribute((const void *)ksgemm::gemm_big3<6>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)ksgemm::gemm_big3_lds()));
     const char *v = getenv("TAE_KS_VALU");
     mfma_ks_ = !(v && v[0] == '1') && p_.pfks_b * 1 <= 16 && p_.ks_b <= 7;
     if (!mfma_ks_) return;
@@ -796,6 +800,22 @@ void Engine::pbs_shift_boolean(const uint64_t *d_small, uint64_t *d_big, size_t 
 void Engine::pfks_into_ggsw(const uint64_t *d_big, uint64_t *d_ggsw, size_t B, int level) {
     if (!B) return;
     const int glwe = (int)p_.glwe_len();
+    if (mfma_ks_ && big_gemm_ && gemm3_) {
+        // digits as 3 balanced 6-bit limbs, limb index in the MFMA row tile (ksgemm.hpp gemm_big3)
+        const int K = p_.K(), kd = (K + 1) * p_.pfks_l;
+        const long mtiles = (long)((B + 63) / 64);
+        ensure_digits(d_digits_, cap_digits_, (size_t)mtiles * ksgemm::B3M, kd, kp_pf_, stream_);
+        const size_t thr = B * (size_t)(K + 1);
+        ksgemm::prep_digits3<6><<<(unsigned)((thr + 255) / 256), 256, 0, stream_>>>(
+            d_big, K + 1, d_digits_, (long)B, K + 1, kp_pf_, p_.pfks_b, p_.pfks_l);
+        const int ncols = (p_.k + 1) * glwe;
+        const long out_stride = (long)p_.cbs_l * ncols;
+        const long ntiles = ((long)ncols * 8 + ksgemm::BTN - 1) / ksgemm::BTN;
+        ksgemm::gemm_big3<6><<<(unsigned)(mtiles * ntiles), 512, ksgemm::gemm_big3_lds(), stream_>>>(
+            d_digits_, d_pf_bt_, kp_pf_, mtiles, ncols, d_ggsw + (size_t)(level - 1) * ncols, out_stride, (long)B);
+        HIPC(hipGetLastError());
+        return;
+    }
     if (mfma_ks_) {
         constexpr int MA = 4, LB = 5;  // 17-bit signed digits as 4 balanced 5-bit limbs
         const int K = p_.K(), kd = (K + 1) * p_.pfks_l;

@@ -351,5 +351,160 @@ __global__ void __launch_bounds__(512, 1)
 
 inline size_t gemm_big_lds() { return (size_t)2 * (BTM + BTN) * LROW; }
 
+// ---- PFKS with 3 balanced 6-bit digit limbs (|d| <= 2^16 fits [-133152, 128991]; every i32 partial
+// sum stays exact: 32 * 128 * 4224 < 2^31), 25% fewer MFMAs than 4 x 5 bits.  The limb index sits in
+// the MFMA row-tile: A row (b, m) = (b / 32) * 96 + 32 m + b % 32, so the 32 x 32 tiles ti = m of a
+// wave hold the three limbs of the same 32 ciphertexts in the same lanes and the epilogue combines
+// them in-lane. ----
+template <int LB3>
+__global__ void __launch_bounds__(256) prep_digits3(const uint64_t *__restrict__ in, long in_stride,
+                                                    int8_t *__restrict__ A, long B, int n_in, int Kp, int base_log,
+                                                    int levels) {
+    const long t = (long)blockIdx.x * 256 + threadIdx.x;
+    const long b = t / n_in;
+    const int i = (int)(t - b * n_in);
+    if (b >= B) return;
+    const uint64_t x = in[b * in_stride + i];
+    const int nrb = 64 - base_log * levels;
+    uint64_t s = x >> (nrb - 1);
+    s += s & 1;
+    s >>= 1;
+    const uint64_t mask = (1ull << base_log) - 1;
+    const long rbase = (b >> 5) * 96 + (b & 31);
+    for (int lev = levels; lev >= 1; lev--) {
+        const uint64_t res = s & mask;
+        s >>= base_log;
+        uint64_t carry = ((res - 1) | s) & res;
+        carry >>= (base_log - 1);
+        s += carry;
+        int32_t d = (int32_t)(res - (carry << base_log));
+        const long kd = (long)i * levels + (lev - 1);
+#pragma unroll
+        for (int m = 0; m < 3; m++) {
+            int32_t limb;
+            if (m == 2) {
+                limb = d;
+            } else {
+                limb = ((d + (1 << (LB3 - 1))) & ((1 << LB3) - 1)) - (1 << (LB3 - 1));
+                d = (d - limb) >> LB3;
+            }
+            A[(rbase + 32 * m) * Kp + kd] = (int8_t)limb;
+        }
+    }
+}
+
+constexpr int B3M = 192;  // rows per workgroup tile: 2 waves x (3 limbs x 32 ciphertexts)
+
+template <int LB3>
+__global__ void __launch_bounds__(512, 1)
+    gemm_big3(const int8_t *__restrict__ A, const int8_t *__restrict__ Bt, int Kp, long mtiles, int ncols,
+              uint64_t *__restrict__ out, long out_stride, long B) {
+    extern __shared__ __align__(16) int8_t smem_g[];
+    auto sA = [&](int b) { return smem_g + b * B3M * LROW; };
+    auto sB = [&](int b) { return smem_g + 2 * B3M * LROW + b * BTN * LROW; };
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int wm = wave >> 2, wn = wave & 3;
+    constexpr long GN = 16;
+    const long ntiles = (((long)ncols * 8) + BTN - 1) / BTN;
+    const long gsz = GN * mtiles;
+    const long ng = blockIdx.x / gsz, rr = blockIdx.x - ng * gsz;
+    const long gw = min(GN, ntiles - ng * GN);
+    const long mt = rr / gw, nt = ng * GN + (rr - (rr / gw) * gw);
+    const long row0 = mt * B3M;
+    const long col8_0 = nt * BTN;
+    const long N8 = (long)ncols * 8;
+    const long Mrows = mtiles * B3M;  // the digit buffer is padded to whole tiles
+
+    // loader: A 192 rows x 8 chunks (3 per thread), B 256 rows x 8 chunks (4 per thread)
+    v4i ra[3], rb[4];
+    auto gload = [&](int k0) {
+#pragma unroll
+        for (int t = 0; t < 3; t++) {
+            const int c = tid + 512 * t, r = c >> 3, kc = c & 7;
+            ra[t] = *reinterpret_cast<const v4i *>(A + (row0 + r) * Kp + k0 + kc * 16);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const int c = tid + 512 * t, r = c >> 3, kc = c & 7;
+            const long br = col8_0 + r;
+            rb[t] = br < N8 ? *reinterpret_cast<const v4i *>(Bt + br * Kp + k0 + kc * 16) : v4i{0, 0, 0, 0};
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int t = 0; t < 3; t++) {
+            const int c = tid + 512 * t, r = c >> 3, kc = c & 7;
+            *reinterpret_cast<v4i *>(&sA(buf)[r * LROW + kc * 16]) = ra[t];
+        }
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const int c = tid + 512 * t, r = c >> 3, kc = c & 7;
+            *reinterpret_cast<v4i *>(&sB(buf)[r * LROW + kc * 16]) = rb[t];
+        }
+    };
+    (void)Mrows;
+
+    v16i acc[3][2];
+#pragma unroll
+    for (int a = 0; a < 3; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++) acc[a][b] = v16i{0};
+
+    const int r = lane & 31, h = lane >> 5;
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    const int nk = Kp / TK;
+    for (int ks = 0; ks < nk; ks++) {
+        const int cur = ks & 1;
+        if (ks + 1 < nk) gload((ks + 1) * TK);
+#pragma unroll
+        for (int kk = 0; kk < TK / 32; kk++) {
+            if (kk == TK / 64 && ks + 1 < nk) lstore(cur ^ 1);
+            v4i fa[3], fb[2];
+#pragma unroll
+            for (int m = 0; m < 3; m++)
+                fa[m] = *reinterpret_cast<const v4i *>(&sA(cur)[(wm * 96 + m * 32 + r) * LROW + kk * 32 + h * 16]);
+#pragma unroll
+            for (int tj = 0; tj < 2; tj++)
+                fb[tj] = *reinterpret_cast<const v4i *>(&sB(cur)[(wn * 64 + tj * 32 + r) * LROW + kk * 32 + h * 16]);
+#pragma unroll
+            for (int m = 0; m < 3; m++)
+#pragma unroll
+                for (int tj = 0; tj < 2; tj++)
+                    acc[m][tj] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[m], fb[tj], acc[m][tj], 0, 0, 0);
+        }
+        if (ks + 1 < nk) __syncthreads();
+    }
+
+    const int j = r & 7;
+    const long b0 = (mt * 2 + wm) * 32;
+#pragma unroll
+    for (int tj = 0; tj < 2; tj++) {
+        const long col = (col8_0 + wn * 64 + tj * 32 + r) >> 3;
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            uint64_t v = 0;
+#pragma unroll
+            for (int m = 0; m < 3; m++) {
+                const int sh = LB3 * m + 8 * j;
+                const uint64_t p = (uint64_t)(int64_t)acc[m][tj][q];
+                v += sh < 64 ? (p << sh) : 0;  // 6 m + 8 j reaches 68
+
+            }
+#pragma unroll
+            for (int x = 1; x < 8; x <<= 1) {
+                const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+                const uint32_t olo = __shfl_xor((int)lo, x, 64), ohi = __shfl_xor((int)hi, x, 64);
+                v += ((uint64_t)ohi << 32) | olo;
+            }
+            const long b = b0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+            if (j == 0 && col < ncols && b < B) out[b * out_stride + col] = 0 - v;
+        }
+    }
+}
+
+inline size_t gemm_big3_lds() { return (size_t)2 * (B3M + BTN) * LROW; }
+
 }  // namespace ksgemm
 }  // namespace tae
