@@ -17,6 +17,14 @@
 namespace tae {
 namespace br1024 {
 
+// progress-based wave priority (see br512x4.hpp): 3 after a barrier, stepping down through a phase
+template <int P>
+__device__ __forceinline__ void s_setprio_c() {
+#ifndef TAE_X4_NORR
+    __builtin_amdgcn_s_setprio(P);
+#endif
+}
+
 constexpr int N = 1024, M = 512, K1 = 3, C = 2, JOBS = C * K1, THREADS = 512;
 
 // a job's lanes are one wave and a wave's LDS operations execute in order: hand-offs inside a job
@@ -122,6 +130,7 @@ __global__ void __launch_bounds__(THREADS, 1)
     cplx accr[K1 * C];
     cplx gv[K1 * K1];
     for (int step = 0; step < steps; step++) {
+        s_setprio_c<2>();
         int e, gstep;
         if (PBS) {
             const uint64_t a = a_next;
@@ -217,6 +226,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                     X[pidx(tt + 64 * kk)] = csel(tt * kk != 0, tv, v[kk]);
                 }
                 wave_sync();
+                if (lev == LEV) s_setprio_c<1>(); else s_setprio_c<2>();
                 // pass 1: points 64 gg + uu + 8 m, w[8 uu kk]
                 {
                     const int gg = tt >> 3, uu = tt & 7;
@@ -230,6 +240,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                     }
                 }
                 wave_sync();
+                if (lev == LEV) s_setprio_c<0>(); else s_setprio_c<1>();
                 // pass 2: points 8 t + m, no twiddles
 #pragma unroll
                 for (int m = 0; m < 8; m++) v[m] = X[pidx(8 * tt + m)];
@@ -238,9 +249,12 @@ __global__ void __launch_bounds__(THREADS, 1)
                 for (int kk = 0; kk < 8; kk++) X[pidx(8 * tt + kk)] = v[kk];
             }
             br512::lds_sync();
+            s_setprio_c<3>();
             // MAC at Fourier position pos: accumulator (q, c) = accr[q * C + c], p ascending
 #pragma unroll
             for (int p = 0; p < K1; p++) {
+                if (p == 1) s_setprio_c<2>();
+                if (p == 2) s_setprio_c<1>();
                 cplx x[C];
 #pragma unroll
                 for (int c = 0; c < C; c++) x[c] = buf[(c * K1 + p) * BUF_STRIDE + pidx(pos)];
@@ -258,6 +272,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                     }
             }
             br512::lds_sync();
+            s_setprio_c<3>();
         }
         // ---- inverse FFT of the MAC results, accumulated into ACC ----
 #pragma unroll
@@ -265,6 +280,7 @@ __global__ void __launch_bounds__(THREADS, 1)
 #pragma unroll
             for (int c = 0; c < C; c++) buf[(c * K1 + q) * BUF_STRIDE + pidx(pos)] = accr[q * C + c];
         br512::lds_sync();
+        s_setprio_c<3>();
         if (fjob) {
             cplx *Y = buf + jb * BUF_STRIDE;
             cplx v[8];
@@ -289,6 +305,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                 for (int m = 0; m < 8; m++) Y[pidx(64 * gg + uu + 8 * m)] = v[m];
             }
             wave_sync();
+            s_setprio_c<2>();
             // inverse pass 0: conj(w[t kk]) on points t + 64 kk, untwist, from_torus, ACC +=
 #pragma unroll
             for (int kk = 0; kk < 8; kk++) {

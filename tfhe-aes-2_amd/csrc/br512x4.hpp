@@ -34,6 +34,44 @@ using br512x2::swap16;
 using br512x2::wave_sync;
 
 constexpr int C = 3, JOBS = C * K1, THREADS = 1024;
+
+// Progress-based wave priority: after every barrier a wave starts at priority 3 and steps down as
+// it completes parts of the phase, so the SIMD arbiter favours the waves that are behind and the
+// four waves of a SIMD reach the next barrier together (oldest-first arbitration otherwise starves
+// the youngest wave, whose tail then runs alone with its latencies exposed).
+#ifndef TAE_X4_NORR
+#define PRIO(n) __builtin_amdgcn_s_setprio(n)
+#else
+#define PRIO(n) \
+    do {        \
+    } while (0)
+#endif
+
+// TAE_X4_PROF (debug builds only): per-phase cycle sums of every wave of workgroup 0, printed at exit
+#ifdef TAE_X4_PROF
+#define PROF_DECL uint64_t prof_[10] = {0}, prof_t_ = clock64();
+#define PROF_T(i)                          \
+    do {                                   \
+        asm volatile("" ::: "memory");     \
+        const uint64_t now_ = clock64();   \
+        prof_[i] += now_ - prof_t_;        \
+        prof_t_ = now_;                    \
+    } while (0)
+#define PROF_SYNC(i)                                                   \
+    do {                                                               \
+        PROF_T(i);                                                     \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");            \
+        PROF_T(9);                                                     \
+        DBG_SYNC();                                                    \
+        PROF_T(8);                                                     \
+    } while (0)
+#else
+#define PROF_DECL
+#define PROF_T(i) \
+    do {          \
+    } while (0)
+#define PROF_SYNC(i) DBG_SYNC()
+#endif
 constexpr int ACC_STRIDE = N;
 
 __device__ __forceinline__ void swap32(cplx &x, cplx &y) {
@@ -75,6 +113,9 @@ __device__ __forceinline__ void mac_level(const cplx *buf, int pos, cplx *accr, 
     constexpr int PI0 = 4 * G, NA = (15 - PI0) < 4 ? (15 - PI0) : 4, Q0 = PI0 / 3;
 #pragma unroll
     for (int p = 0; p < K1; p++) {
+        if (p == 1) PRIO(2);
+        if (p == 2) PRIO(1);
+        if (p == 3) PRIO(0);
         cplx x[C];
 #pragma unroll
         for (int c = 0; c < C; c++) x[c] = buf[(c * K1 + p) * BUF_STRIDE + pos];
@@ -182,6 +223,7 @@ __global__ void __launch_bounds__(THREADS, 1)
     cplx accr[4];
     cplx gv[K1 * 2];
     const cplx *my_w16 = s_w16 + 3 * r;
+    PROF_DECL
     for (int step = 0; step < steps; step++) {
         int e, gstep;
         if (PBS) {
@@ -207,6 +249,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                     }
                 }
         };
+        PRIO(2);
         // ---- rotated difference + decomposition of coefficients j = u + 16 r + 64 i (+ M) ----
         int ll = lane;
         asm volatile("" : "+v"(ll));
@@ -241,6 +284,8 @@ __global__ void __launch_bounds__(THREADS, 1)
         }
 #pragma unroll
         for (int a = 0; a < 4; a++) accr[a] = cplx{0.0, 0.0};
+        PRIO(2);
+        PROF_T(0);
 
 #pragma unroll
         for (int lev = LEV; lev >= 1; lev--) {
@@ -263,6 +308,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                     v[i] = {fma(a0, tw.re, -(a1 * tw.im)), fma(a0, tw.im, a1 * tw.re)};
                 }
                 dft16x4<false>(v, my_w16);
+                if (lev == LEV) PRIO(1); else PRIO(2);
                 cplx *dst = buf + jb * BUF_STRIDE;
 #pragma unroll
                 for (int k2 = 0; k2 < 4; k2++) {
@@ -271,6 +317,8 @@ __global__ void __launch_bounds__(THREADS, 1)
                 }
             }
             wave_sync();
+            PRIO(1);
+            PROF_T(1);
             // pass B (row u): DFT16 over positions 16 u + r + 4 i, in place
             if (fjob) {
                 cplx *base = buf + jb * BUF_STRIDE;
@@ -278,10 +326,12 @@ __global__ void __launch_bounds__(THREADS, 1)
 #pragma unroll
                 for (int i = 0; i < 4; i++) v[i] = base[pidx(16 * u + r + 4 * i)];
                 dft16x4<false>(v, my_w16);
+                PRIO(0);
 #pragma unroll
                 for (int k2 = 0; k2 < 4; k2++) base[pidx(16 * u + r + 4 * k2)] = v[k2];
             }
-            DBG_SYNC();
+            PROF_SYNC(2);
+            PRIO(3);
 #ifndef TAE_DBG_NOMAC
             switch (grp) {
             case 0: mac_level<0>(buf, pidx(pos), accr, gv); break;
@@ -290,7 +340,8 @@ __global__ void __launch_bounds__(THREADS, 1)
             default: mac_level<3>(buf, pidx(pos), accr, gv); break;
             }
 #endif
-            DBG_SYNC();
+            PROF_SYNC(3);
+            PRIO(3);
         }
         // ---- inverse FFT of the MAC results, accumulated into ACC ----
         switch (grp) {
@@ -299,7 +350,8 @@ __global__ void __launch_bounds__(THREADS, 1)
         case 2: mac_store<2>(buf, pidx(pos), accr); break;
         default: mac_store<3>(buf, pidx(pos), accr); break;
         }
-        DBG_SYNC();
+        PROF_SYNC(4);
+        PRIO(3);
         if (fjob) {  // pass B^-1 (row u)
             cplx *base = buf + jb * BUF_STRIDE;
             cplx v[4];
@@ -310,6 +362,8 @@ __global__ void __launch_bounds__(THREADS, 1)
             for (int k2 = 0; k2 < 4; k2++) base[pidx(16 * u + r + 4 * k2)] = v[k2];
         }
         wave_sync();
+        PRIO(3);
+        PROF_T(5);
         if (fjob) {  // pass A^-1 (column u): conj(W_M^{u kk}), DFT16^-1 over kk, untwist, from_torus, ACC +=
             const cplx *src = buf + jb * BUF_STRIDE;
             cplx v[4];
@@ -334,7 +388,16 @@ __global__ void __launch_bounds__(THREADS, 1)
             }
         }
         wave_sync();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        PROF_T(6);
     }
+#ifdef TAE_X4_PROF
+    if (blockIdx.x == 0 && lane == 0)
+        printf("x4prof wave %2d: dec %llu passA %llu passB %llu mac %llu store %llu invB %llu invA %llu bar %llu lgkm %llu\n",
+               jb, (unsigned long long)prof_[0], (unsigned long long)prof_[1], (unsigned long long)prof_[2],
+               (unsigned long long)prof_[3], (unsigned long long)prof_[4], (unsigned long long)prof_[5],
+               (unsigned long long)prof_[6], (unsigned long long)prof_[8], (unsigned long long)prof_[9]);
+#endif
     lds_sync();  // sample extraction reads every job's ACC
     for (int ct = 0; ct < nct; ct++) {
         const uint64_t *a = acc + ct * K1 * ACC_STRIDE;

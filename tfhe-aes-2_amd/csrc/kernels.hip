@@ -20,6 +20,7 @@
 #include "br512.hpp"
 #include "br512x2.hpp"
 #include "br512x4.hpp"
+#include "br512x5.hpp"
 #include "br1024.hpp"
 #include "ksgemm.hpp"
 #include "engine.hpp"
@@ -582,7 +583,15 @@ void Engine::init_common() {
     // 1024-thread kernel (br512x4.hpp) by default; TAE_BR_X2=1 keeps the 512-thread one
     const char *bx2 = getenv("TAE_BR_X2");
     x4_512_ = wide512_ && !(bx2 && bx2[0] == '1') && p_.pbs_b == 12 && p_.cbs_b == 13;
+    // register-ACC / double-buffered variant (br512x5.hpp), opt-in with TAE_BR_X5=1: it needs more
+    // than the 128 VGPRs of 4 waves per SIMD and spills (295 ms vs 205 ms per PBS launch)
+    const char *bx5 = getenv("TAE_BR_X5");
+    x5_512_ = x4_512_ && bx5 && bx5[0] == '1';
     if (batched512_) {
+        HIPC(hipFuncSetAttribute((const void *)br512x5::br_kernel<3, true, 12>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        HIPC(hipFuncSetAttribute((const void *)br512x5::br_kernel<1, false, 13>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         HIPC(hipFuncSetAttribute((const void *)br512x4::br_kernel<3, true, 12>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         HIPC(hipFuncSetAttribute((const void *)br512x4::br_kernel<1, false, 13>,
@@ -753,6 +762,12 @@ void Engine::bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint
     if (batched512_ && p_.pbs_l == 3) {
         const br512::W16 W = make_w16(w16_);
         const size_t wgs = (B + kBrC - 1) / kBrC;
+        if (x5_512_) {
+            br512x5::br_kernel<3, true, 12><<<(unsigned)wgs, br512x5::THREADS, br512x5::lds_bytes(), stream_>>>(
+                d_small, p_.n, d_lut_glwe, 0, d_bsk_f_, 0, d_big, (long)B, body_add, out_add, d_twist_, d_w_);
+            HIPC(hipGetLastError());
+            return;
+        }
         if (x4_512_) {
             br512x4::br_kernel<3, true, 12><<<(unsigned)wgs, br512x4::THREADS, br512x4::lds_bytes(), stream_>>>(
                 d_small, p_.n, d_lut_glwe, 0, d_bsk_f_, 0, d_big, (long)B, body_add, out_add, d_twist_, d_w_);
@@ -873,6 +888,12 @@ void Engine::vertical_packing(const cplx *d_ggsw_f, size_t G, int n_in, const ui
     if (batched512_ && p_.cbs_l == 1) {
         const br512::W16 W = make_w16(w16_);
         const size_t wgs = G * (size_t)((n_out + kBrC - 1) / kBrC);
+        if (x5_512_) {
+            br512x5::br_kernel<1, false, 13><<<(unsigned)wgs, br512x5::THREADS, br512x5::lds_bytes(), stream_>>>(
+                nullptr, 0, d_lut, n_out, d_ggsw_f, n_in, d_out, (long)G, 0, 0, d_twist_, d_w_);
+            HIPC(hipGetLastError());
+            return;
+        }
         if (x4_512_) {
             br512x4::br_kernel<1, false, 13><<<(unsigned)wgs, br512x4::THREADS, br512x4::lds_bytes(), stream_>>>(
                 nullptr, 0, d_lut, n_out, d_ggsw_f, n_in, d_out, (long)G, 0, 0, d_twist_, d_w_);
