@@ -101,12 +101,34 @@ def test_increment_8bit_adder(keys):
     assert got == [0, 1, 2]
 
 
-def test_cmux_tree_lut_rejected_on_device(keys):
+def test_cmux_tree_lut_bit_exact(keys, oracle_keys):
+    """A LUT with 10 > log2(512) inputs (generate_lookup_table :274-289 with a WopbsLUTBase of 2
+    polynomials per output): the device CMux tree over the first GGSW, then the blind rotation over
+    the other 9 (tfhe-rs vertical_packing), equal to the oracle and decrypting to f(word)."""
     ck, ctx = keys
-    lut = ctx.generate_lookup_table(10, 1, lambda v: v & 1)  # 10 > log2(512): needs the CMux tree
-    cts = [ck.encrypt(Cleartext(0)) for _ in range(10)]
-    with pytest.raises(tfhe_aes.TaeError):
-        ctx.circuit_bootstrap(cts, lut)
+    f = lambda v: ((v * 37) ^ (v >> 3)) & 7
+    lut = ctx.generate_lookup_table(10, 3, f)
+    for word, start in ((0b1011001110, 70_000), (0b0100110001, 70_100)):
+        cts = ck.encrypt_bits_raw([(word >> (9 - i)) & 1 for i in range(10)], start_index=start)
+        out = ctx.circuit_bootstrap_raw(cts.reshape(1, 10, -1), lut)
+        got = ck.decrypt_bits_raw(out[0])
+        assert [int(b) for b in got] == [(f(word) >> (2 - j)) & 1 for j in range(3)], bin(word)
+    assert np.array_equal(out[0], oracle_keys.circuit_bootstrap(cts, lut.as_array(), 3))
+
+
+def test_multivariate_multivalues_xor_8bit():
+    """test_multivariate_multivalues_xor_8bit (:626-659): params_sqrd_lvl_1 (N = 1024), a 16 -> 8 LUT
+    b1 ^ b2 over a 64-polynomial WopbsLUTBase (6-level CMux tree + 10-step blind rotation)."""
+    from tests.conftest import SEED
+    ck, keys_raw = tfhe_aes.generate_keys_raw(tfhe_aes.PARAMS_SQRD_LVL_1, SEED, threads=16)
+    ctx = tfhe_aes.context_from_raw(tfhe_aes.PARAMS_SQRD_LVL_1, keys_raw, device=0)
+    b1, b2 = 0b11000110, 0b10101010
+    word = (b1 << 8) | b2
+    xor_fn = lambda v: (v >> 8) ^ (v & 0xFF)
+    tv = ctx.generate_lookup_table(16, 8, xor_fn)
+    bits = [ck.encrypt(Cleartext(b)) for b in u16_to_bits(word)]
+    out = ctx.circuit_bootstrap(bits, tv)
+    assert aes_128.bits_to_u8([ck.decrypt(b).value for b in out]) == xor_fn(word)
 
 
 def test_light_gal_mul(keys, golden):

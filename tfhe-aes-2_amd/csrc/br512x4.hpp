@@ -289,10 +289,10 @@ __global__ void __launch_bounds__(THREADS, 1)
 
 #pragma unroll
         for (int lev = LEV; lev >= 1; lev--) {
-#ifndef TAE_DBG_NOGLOAD
-            load_level(lev);
-#else
+#if defined(TAE_DBG_NOGLOAD)
             if (lev == LEV) load_level(lev);
+#elif !defined(TAE_X4_G_MID) && !defined(TAE_X4_G_LATE)
+            load_level(lev);
 #endif
             // pass A (column u): twist, DFT16 over m = r + 4 i, W_M^{u k} -> LDS position u + 16 k
             if (fjob) {
@@ -318,6 +318,9 @@ __global__ void __launch_bounds__(THREADS, 1)
             }
             wave_sync();
             PRIO(1);
+#ifdef TAE_X4_G_MID
+            load_level(lev);
+#endif
             PROF_T(1);
             // pass B (row u): DFT16 over positions 16 u + r + 4 i, in place
             if (fjob) {
@@ -330,6 +333,9 @@ __global__ void __launch_bounds__(THREADS, 1)
 #pragma unroll
                 for (int k2 = 0; k2 < 4; k2++) base[pidx(16 * u + r + 4 * k2)] = v[k2];
             }
+#ifdef TAE_X4_G_LATE
+            load_level(lev);
+#endif
             PROF_SYNC(2);
             PRIO(3);
 #ifndef TAE_DBG_NOMAC

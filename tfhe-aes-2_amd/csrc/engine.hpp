@@ -65,6 +65,9 @@ class Engine {
     // [n_out][N], out [G][n_out][K+1]
     void vertical_packing(const cplx *d_ggsw_f, size_t G, int n_in, const uint64_t *d_lut, int n_out,
                           uint64_t *d_out);
+    // LUTs with input_bits > log2 N: CMux tree over the first `tree` GGSWs, then the blind rotation
+    void vertical_packing_tree(const cplx *d_ggsw_f, size_t G, int n_in, int tree, const uint64_t *d_lut, int n_out,
+                               uint64_t *d_out);
     // FheContext::circuit_bootstrap over G groups: bits [G][n_in][K+1] -> [G][n_out][K+1]
     void circuit_bootstrap(const uint64_t *d_bits, size_t G, int n_in, const uint64_t *d_lut,
                            int n_out, uint64_t *d_out);

@@ -40,6 +40,7 @@ constexpr int kThreads = 256;
 // ---------------------------------------------------------------------------------------------
 // External product on an LDS-resident GLWE accumulator:
 //   acc += GGSW [x] (acc * X^e - acc)          (cmux(ct0 = acc, ct1 = acc * X^e, ggsw))
+// or, with ct1 given (the CMux tree of vertical packing), acc += GGSW [x] (ct1 - acc).
 // GGSW Fourier layout [lev-1][row p][col c][M]; rows consumed finest level first, p ascending
 // (fft64 add_external_product_assign: ggsw.into_levels().rev() zipped with the decomposition).
 // ---------------------------------------------------------------------------------------------
@@ -47,7 +48,7 @@ template <int N>
 __device__ void ext_product_step(uint64_t *__restrict__ acc, cplx *__restrict__ X, cplx *__restrict__ Y,
                                  int e, const cplx *__restrict__ ggsw, int k, int levels, int base_log,
                                  const cplx *__restrict__ twist, const cplx *__restrict__ untwist,
-                                 const cplx *__restrict__ w) {
+                                 const cplx *__restrict__ w, const uint64_t *__restrict__ ct1 = nullptr) {
     constexpr int M = N / 2;
     constexpr int R = FftPlan<M>::R, P = FftPlan<M>::P, TPJ = M / R;
     const int tid = threadIdx.x;
@@ -62,8 +63,9 @@ __device__ void ext_product_step(uint64_t *__restrict__ acc, cplx *__restrict__ 
 #pragma unroll
             for (int m = 0; m < R; m++) {
                 const int j = u + m * TPJ;
-                const uint64_t d0 = rotated_coeff(poly, j, e, N) - poly[j];
-                const uint64_t d1 = rotated_coeff(poly, j + M, e, N) - poly[j + M];
+                const uint64_t *c1 = ct1 ? ct1 + p * N : nullptr;
+                const uint64_t d0 = (c1 ? c1[j] : rotated_coeff(poly, j, e, N)) - poly[j];
+                const uint64_t d1 = (c1 ? c1[j + M] : rotated_coeff(poly, j + M, e, N)) - poly[j + M];
                 const double x0 = (double)decomp_digit(d0, base_log, levels, lev);
                 const double x1 = (double)decomp_digit(d1, base_log, levels, lev);
                 const cplx t = twist[j];
@@ -198,31 +200,82 @@ __global__ void __launch_bounds__(kThreads) pbs_kernel(const uint64_t *__restric
 }
 
 // ---------------------------------------------------------------------------------------------
-// Vertical packing (no CMux tree): workgroup (group g, output j): ACC = trivial(LUT_j); for the
-// GGSWs in reverse order, cmux(ACC, ACC * X^{-2^t}, GGSW); extract coefficient 0.
-// (wop_pbs::vertical_packing -> blind_rotate_assign)
+// Vertical packing: workgroup (group g, output j): ACC = trivial(LUT_j), or the CMux tree's GLWE
+// init[g][j] when the LUT has more than one polynomial; for the GGSWs n_in-1 .. b_stop,
+// cmux(ACC, ACC * X^{-2^t}, GGSW); extract coefficient 0.  (wop_pbs::vertical_packing ->
+// blind_rotate_assign)
 // ---------------------------------------------------------------------------------------------
 template <int N>
 __global__ void __launch_bounds__(kThreads) vp_kernel(const cplx *__restrict__ ggsw_f, int n_in, const uint64_t *__restrict__ lut,
                                                    int n_out, uint64_t *__restrict__ out, const cplx *__restrict__ twist,
                                                    const cplx *__restrict__ untwist, const cplx *__restrict__ w, int k,
-                                                   int levels, int base_log) {
+                                                   int levels, int base_log, const uint64_t *__restrict__ init = nullptr,
+                                                   int b_stop = 0) {
     constexpr int M = N / 2;
     extern __shared__ __align__(16) unsigned char smem[];
     uint64_t *acc = reinterpret_cast<uint64_t *>(smem);
     cplx *X = reinterpret_cast<cplx *>(acc + (k + 1) * N);
     cplx *Y = X + (k + 1) * M;
     const int g = blockIdx.x / n_out, jout = blockIdx.x - g * n_out;
-    for (int t = threadIdx.x; t < (k + 1) * N; t += blockDim.x) acc[t] = t < k * N ? 0 : lut[(size_t)jout * N + (t - k * N)];
+    if (init) {
+        const uint64_t *src = init + (size_t)blockIdx.x * (k + 1) * N;
+        for (int t = threadIdx.x; t < (k + 1) * N; t += blockDim.x) acc[t] = src[t];
+    } else {
+        for (int t = threadIdx.x; t < (k + 1) * N; t += blockDim.x)
+            acc[t] = t < k * N ? 0 : lut[(size_t)jout * N + (t - k * N)];
+    }
     __syncthreads();
     const size_t ggsw_sz = (size_t)levels * (k + 1) * (k + 1) * M;
     int deg = 1;
-    for (int b = n_in - 1; b >= 0; b--, deg <<= 1) {
+    for (int b = n_in - 1; b >= b_stop; b--, deg <<= 1) {
         const int e = 2 * N - deg;
         ext_product_step<N>(acc, X, Y, e, ggsw_f + ((size_t)g * n_in + b) * ggsw_sz, k, levels, base_log, twist,
                             untwist, w);
     }
     sample_extract_store<N>(acc, k, 0, out + ((size_t)g * n_out + jout) * (k * N + 1));
+}
+
+// ---------------------------------------------------------------------------------------------
+// CMux tree of vertical packing (wop_pbs cmux_tree_memory_optimized) for LUTs of 2^tree
+// polynomials (input_bits > log2 N).  Leaves: trivial GLWEs of the LUT polynomials,
+// [n_out][2^tree][(k+1)N], shared by every group.  One tree level: workgroup (g, j, i) computes
+// node i = cmux(c0 = src[g][j][2i], c1 = src[g][j][2i+1], GGSW_{g, t}) = c0 + GGSW [x] (c1 - c0).
+// ---------------------------------------------------------------------------------------------
+__global__ void vp_leaves_kernel(const uint64_t *__restrict__ lut, size_t small_len, int n_out, int cnt, int k, int N,
+                                 uint64_t *__restrict__ leaves) {
+    const size_t glwe = (size_t)(k + 1) * N;
+    const size_t total = (size_t)n_out * cnt * glwe;
+    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
+        const size_t row = t / glwe, c = t - row * glwe;
+        const size_t j = row / cnt, i = row - j * cnt;
+        leaves[t] = c < (size_t)k * N ? 0 : lut[j * small_len + i * N + (c - (size_t)k * N)];
+    }
+}
+
+template <int N>
+__global__ void __launch_bounds__(kThreads) cmux_tree_kernel(const cplx *__restrict__ ggsw_f, int n_in, int t,
+                                                          const uint64_t *__restrict__ src, long src_gstride, int cnt,
+                                                          int n_out, uint64_t *__restrict__ dst,
+                                                          const cplx *__restrict__ twist, const cplx *__restrict__ untwist,
+                                                          const cplx *__restrict__ w, int k, int levels, int base_log) {
+    constexpr int M = N / 2;
+    extern __shared__ __align__(16) unsigned char smem[];
+    uint64_t *acc = reinterpret_cast<uint64_t *>(smem);
+    cplx *X = reinterpret_cast<cplx *>(acc + (k + 1) * N);
+    cplx *Y = X + (k + 1) * M;
+    const size_t glwe = (size_t)(k + 1) * N;
+    const int half = cnt / 2;
+    const size_t gj = blockIdx.x / half;
+    const int i = (int)(blockIdx.x - gj * half);
+    const size_t g = gj / n_out, j = gj - g * n_out;
+    const uint64_t *c0 = src + g * src_gstride + (j * cnt + 2 * i) * glwe;
+    for (int x = threadIdx.x; x < (int)glwe; x += blockDim.x) acc[x] = c0[x];
+    __syncthreads();
+    const size_t ggsw_sz = (size_t)levels * (k + 1) * (k + 1) * M;
+    ext_product_step<N>(acc, X, Y, 0, ggsw_f + (g * n_in + t) * ggsw_sz, k, levels, base_log, twist, untwist, w,
+                        c0 + glwe);
+    uint64_t *o = dst + (gj * half + i) * glwe;
+    for (int x = threadIdx.x; x < (int)glwe; x += blockDim.x) o[x] = acc[x];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -618,9 +671,11 @@ void Engine::init_common() {
     if (p_.N == 512) {
         HIPC(hipFuncSetAttribute((const void *)pbs_kernel<512>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         HIPC(hipFuncSetAttribute((const void *)vp_kernel<512>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        HIPC(hipFuncSetAttribute((const void *)cmux_tree_kernel<512>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     } else {
         HIPC(hipFuncSetAttribute((const void *)pbs_kernel<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         HIPC(hipFuncSetAttribute((const void *)vp_kernel<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        HIPC(hipFuncSetAttribute((const void *)cmux_tree_kernel<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     }
 }
 
@@ -879,12 +934,57 @@ void Engine::ggsw_to_fourier(const uint64_t *d_ggsw, cplx *d_ggsw_f, size_t B) {
     HIPC(hipGetLastError());
 }
 
+// LUTs with 2^tree polynomials: the CMux tree over GGSWs tree-1 .. 0 (tfhe-rs order: the first
+// `tree` GGSWs select the polynomial), then the blind rotation over GGSWs n_in-1 .. tree on the
+// generic kernels (oracle: or_vertical_packing).
+void Engine::vertical_packing_tree(const cplx *d_ggsw_f, size_t G, int n_in, int tree, const uint64_t *d_lut,
+                                   int n_out, uint64_t *d_out) {
+    const size_t glwe = p_.glwe_len(), cnt0 = (size_t)1 << tree, small_len = (size_t)p_.N << tree;
+    uint64_t *leaves = nullptr, *lv[2] = {nullptr, nullptr};
+    HIPC(hipMallocAsync((void **)&leaves, (size_t)n_out * cnt0 * glwe * 8, stream_));
+    HIPC(hipMallocAsync((void **)&lv[0], G * n_out * (cnt0 / 2) * glwe * 8, stream_));
+    if (cnt0 >= 4) HIPC(hipMallocAsync((void **)&lv[1], G * n_out * (cnt0 / 4) * glwe * 8, stream_));
+    vp_leaves_kernel<<<1024, 256, 0, stream_>>>(d_lut, small_len, n_out, (int)cnt0, p_.k, p_.N, leaves);
+    HIPC(hipGetLastError());
+    const uint64_t *src = leaves;
+    long gstride = 0;
+    int cnt = (int)cnt0, buf = 0;
+    for (int t = tree - 1; t >= 0; t--, cnt /= 2, buf ^= 1) {
+        const unsigned wgs = (unsigned)(G * n_out * (size_t)(cnt / 2));
+        if (p_.N == 512)
+            cmux_tree_kernel<512><<<wgs, kThreads, br_lds_bytes<512>(p_.k, p_.cbs_l), stream_>>>(
+                d_ggsw_f, n_in, t, src, gstride, cnt, n_out, lv[buf], d_twist_, d_untwist_, d_w_, p_.k, p_.cbs_l,
+                p_.cbs_b);
+        else
+            cmux_tree_kernel<1024><<<wgs, kThreads, br_lds_bytes<1024>(p_.k, p_.cbs_l), stream_>>>(
+                d_ggsw_f, n_in, t, src, gstride, cnt, n_out, lv[buf], d_twist_, d_untwist_, d_w_, p_.k, p_.cbs_l,
+                p_.cbs_b);
+        HIPC(hipGetLastError());
+        src = lv[buf];
+        gstride = (long)(n_out * (size_t)(cnt / 2) * glwe);
+    }
+    const unsigned wgs = (unsigned)(G * (size_t)n_out);
+    if (p_.N == 512)
+        vp_kernel<512><<<wgs, kThreads, br_lds_bytes<512>(p_.k, p_.cbs_l), stream_>>>(
+            d_ggsw_f, n_in, d_lut, n_out, d_out, d_twist_, d_untwist_, d_w_, p_.k, p_.cbs_l, p_.cbs_b, src, tree);
+    else
+        vp_kernel<1024><<<wgs, kThreads, br_lds_bytes<1024>(p_.k, p_.cbs_l), stream_>>>(
+            d_ggsw_f, n_in, d_lut, n_out, d_out, d_twist_, d_untwist_, d_w_, p_.k, p_.cbs_l, p_.cbs_b, src, tree);
+    HIPC(hipGetLastError());
+    HIPC(hipFreeAsync(leaves, stream_));
+    HIPC(hipFreeAsync(lv[0], stream_));
+    if (lv[1]) HIPC(hipFreeAsync(lv[1], stream_));
+}
+
 void Engine::vertical_packing(const cplx *d_ggsw_f, size_t G, int n_in, const uint64_t *d_lut, int n_out,
                               uint64_t *d_out) {
     if (!G) return;
     int logN = 0;
     while ((1 << logN) < p_.N) logN++;
-    if (n_in > logN) throw std::runtime_error("vertical packing with a CMux tree (input_bits > log2 N) is not supported on device");
+    if (n_in > logN) {
+        vertical_packing_tree(d_ggsw_f, G, n_in, n_in - logN, d_lut, n_out, d_out);
+        return;
+    }
     if (batched512_ && p_.cbs_l == 1) {
         const br512::W16 W = make_w16(w16_);
         const size_t wgs = G * (size_t)((n_out + kBrC - 1) / kBrC);

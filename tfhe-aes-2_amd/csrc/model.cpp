@@ -239,8 +239,6 @@ void Context::circuit_bootstrap_raw(const uint64_t *bits, size_t groups, int n_i
              &lut);
         return;
     }
-    if (lut.small_len != (size_t)params().N)
-        throw ModelError{TAE_E_PARAM, "LUTs with input_bits > log2(N) need the CMux tree (not on device yet)"};
     std::lock_guard<std::mutex> g(mu_);
     const size_t L = params().big_len();
     hip_check(hipSetDevice(engine_->device()), "hipSetDevice");
