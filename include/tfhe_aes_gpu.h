@@ -87,6 +87,21 @@ int tae_client_key_from_seed(int param_set, const uint8_t seed[32], tae_client_k
 int tae_context_create_raw(int param_set, int device, const uint64_t *ksk, const uint64_t *bsk,
                            const uint64_t *pfpksk, int mem, tae_context **context);
 void tae_context_free(tae_context *ctx);
+
+/* ---- On-disk keys (no reference counterpart: the reference keeps keys in memory) --
+ * One little-endian file "TAEKEY01" holding a client key (its 32-byte seed + encryption counter)
+ * and/or the standard-domain server keys (ksk, bsk, pfpksk as sized by tae_server_key_sizes), with
+ * a trailing checksum (format: tfhe-aes-2_amd/csrc/keyio.cpp).  Rejected files -> TAE_E_ARG. */
+#define TAE_KEYS_CLIENT 1
+#define TAE_KEYS_SERVER 2
+/* client_key may be NULL; ksk/bsk/pfpksk all NULL (client only) or all set */
+int tae_keys_save(const char *path, int param_set, const tae_client_key *client_key, const uint64_t *ksk,
+                  const uint64_t *bsk, const uint64_t *pfpksk);
+/* parameter set and TAE_KEYS_* flags from the header (payload not verified) */
+int tae_keys_file_info(const char *path, int *param_set, int *flags);
+/* client_key (NULL: not wanted) and/or the three server arrays (all NULL: not wanted); the checksum
+ * is verified before anything is returned (server arrays are filled in place: discard them on error) */
+int tae_keys_load(const char *path, tae_client_key **client_key, uint64_t *ksk, uint64_t *bsk, uint64_t *pfpksk);
 void tae_client_key_free(tae_client_key *ck);
 int tae_client_key_secrets(const tae_client_key *ck, uint64_t *lwe_sk /*[n]*/,
                            uint64_t *glwe_sk /*[k*N]*/);

@@ -13,7 +13,7 @@ done
 wait
 for spec in "$@"; do
   name=${spec%%=*}
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o dbg/$name.so dbg/$name.o build/client.o build/model.o build/capi.o -lpthread
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o dbg/$name.so dbg/$name.o build/client.o build/model.o build/capi.o build/keyio.o -lpthread
   rm dbg/$name.o
 done
 ls dbg

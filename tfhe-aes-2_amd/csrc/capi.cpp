@@ -199,6 +199,52 @@ int tae_client_key_from_seed(int param_set, const uint8_t seed[32], tae_client_k
     });
 }
 
+extern "C++" {
+namespace tae {
+namespace keyio {
+void save(const char *path, const Params &p, int param_set, const ClientKey *ck, const uint64_t *ksk,
+          const uint64_t *bsk, const uint64_t *pfpksk);
+void load(const char *path, int *param_set, uint32_t *flags, ClientKey *ck, uint64_t *ksk, uint64_t *bsk,
+          uint64_t *pfpksk);
+}  // namespace keyio
+}  // namespace tae
+}
+
+int tae_keys_save(const char *path, int param_set, const tae_client_key *client_key, const uint64_t *ksk,
+                  const uint64_t *bsk, const uint64_t *pfpksk) {
+    return guarded([&] {
+        require(path, "null path");
+        const tae::Params p = params_of(param_set);
+        if (client_key) {
+            const tae::Params &q = client_key->ck.p;
+            require(q.n == p.n && q.k == p.k && q.N == p.N && q.model == p.model,
+                    "client key does not belong to the parameter set");
+        }
+        tae::keyio::save(path, p, param_set, client_key ? &client_key->ck : nullptr, ksk, bsk, pfpksk);
+    });
+}
+
+int tae_keys_file_info(const char *path, int *param_set, int *flags) {
+    return guarded([&] {
+        require(path && param_set && flags, "null argument");
+        uint32_t fl = 0;
+        tae::keyio::load(path, param_set, &fl, nullptr, nullptr, nullptr, nullptr);
+        *flags = (int)fl;
+    });
+}
+
+int tae_keys_load(const char *path, tae_client_key **client_key, uint64_t *ksk, uint64_t *bsk, uint64_t *pfpksk) {
+    return guarded([&] {
+        require(path, "null path");
+        require(client_key || ksk || bsk || pfpksk, "nothing to load");
+        int ps = 0;
+        uint32_t fl = 0;
+        std::unique_ptr<tae_client_key> ck = client_key ? std::make_unique<tae_client_key>() : nullptr;
+        tae::keyio::load(path, &ps, &fl, ck ? &ck->ck : nullptr, ksk, bsk, pfpksk);
+        if (client_key) *client_key = ck.release();
+    });
+}
+
 int tae_context_create_raw(int param_set, int device, const uint64_t *ksk, const uint64_t *bsk,
                            const uint64_t *pfpksk, int mem, tae_context **context) {
     return guarded([&] {

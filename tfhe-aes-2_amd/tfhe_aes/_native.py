@@ -30,8 +30,9 @@ EXPORTED = [
     "tae_stage_bootstrap", "tae_stage_pfks_ggsw", "tae_stage_ggsw_fourier", "tae_stage_vertical_packing",
     "tae_synchronize", "tae_set_timing", "tae_last_stage_times", "tae_bit_len", "tae_encrypt_ints_raw",
     "tae_decrypt_ints_raw", "tae_bootstrap_from_bits_raw", "tae_extract_bits_raw", "tae_aes_key_schedule_raw",
-    "tae_last_stage_times_v2",
+    "tae_last_stage_times_v2", "tae_keys_save", "tae_keys_file_info", "tae_keys_load",
 ]
+TAE_KEYS_CLIENT, TAE_KEYS_SERVER = 1, 2
 
 
 class TaeParams(C.Structure):
@@ -119,6 +120,9 @@ def lib() -> C.CDLL:
         "tae_extract_bits_raw": ([vp, vp, sz, vp, C.c_int], C.c_int),
         "tae_aes_key_schedule_raw": ([vp, vp, vp, C.c_int], C.c_int),
         "tae_last_stage_times_v2": ([vp, C.POINTER(C.c_float)], C.c_int),
+        "tae_keys_save": ([C.c_char_p, C.c_int, vp, vp, vp, vp], C.c_int),
+        "tae_keys_file_info": ([C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int)], C.c_int),
+        "tae_keys_load": ([C.c_char_p, vpp, vp, vp, vp], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -308,3 +308,37 @@ def context_from_raw(param_set: int, keys, device: int = 0, mem: int = N.TAE_MEM
     ctx = C.c_void_p()
     check(lib().tae_context_create_raw(param_set, device, ptrs[0], ptrs[1], ptrs[2], mem, C.byref(ctx)))
     return FheContext(ctx.value, param_set)
+
+
+# ---- on-disk keys (include/tfhe_aes_gpu.h tae_keys_*; format in csrc/keyio.cpp) ----
+def save_keys(path, param_set: int, client_key: "ClientKey | None" = None, server_keys=None) -> None:
+    """Write a TAEKEY01 file with the client key (seed + encryption counter) and/or the raw server
+    keys (ksk, bsk, pfpksk) as returned by generate_keys_raw."""
+    ptrs = [None, None, None]
+    if server_keys is not None:
+        arrs = [np.ascontiguousarray(k, dtype=np.uint64) for k in server_keys]
+        ptrs = [a.ctypes.data_as(C.c_void_p) for a in arrs]
+    check(lib().tae_keys_save(os.fsencode(path), param_set, client_key._h if client_key else None, *ptrs))
+
+
+def key_file_info(path) -> tuple:
+    """(param_set, has_client_key, has_server_keys) from the file header."""
+    ps, fl = C.c_int(), C.c_int()
+    check(lib().tae_keys_file_info(os.fsencode(path), C.byref(ps), C.byref(fl)))
+    return ps.value, bool(fl.value & N.TAE_KEYS_CLIENT), bool(fl.value & N.TAE_KEYS_SERVER)
+
+
+def load_keys(path, client: bool = True, server: bool = True):
+    """(client_key or None, (ksk, bsk, pfpksk) or None) from a TAEKEY01 file; the checksum is
+    verified before anything is returned."""
+    param_set, has_ck, has_sk = key_file_info(path)
+    client, server = client and has_ck, server and has_sk
+    ptrs, arrs = [None, None, None], None
+    if server:
+        sizes = [C.c_size_t() for _ in range(3)]
+        check(lib().tae_server_key_sizes(param_set, *[C.byref(s) for s in sizes]))
+        arrs = tuple(np.empty(s.value, dtype=np.uint64) for s in sizes)
+        ptrs = [a.ctypes.data_as(C.c_void_p) for a in arrs]
+    ck = C.c_void_p()
+    check(lib().tae_keys_load(os.fsencode(path), C.byref(ck) if client else None, *ptrs))
+    return (ClientKey(ck.value, param_set) if client else None), arrs
