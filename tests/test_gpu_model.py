@@ -178,3 +178,20 @@ def test_readme_counter_mode_batched(keys, golden):
     out = aes_128.ShortintWoppbs1BitSboxGalMulPbsAesEncrypt.encrypt_blocks_raw(ctx, rk, cts, rounds=10)
     got = [b.hex() for b in aes_128.bits_to_blocks(ck.decrypt_bits_raw(out))]
     assert got == [g["ciphertexts"][str(c)] for c in range(1, 11)]
+
+
+def test_sbox_pbs_driver_on_1bit_model_trips_noise_bookkeeping(keys, golden):
+    """ShortintWoppbs1BitSboxPbsAesEncrypt (fhe_impls/shortint_woppbs_1bit.rs:47-81): its reference
+    tests test_light / test_full are #[ignore]d because the leveled MixColumns of fhe_sbox_pbs breaks
+    the BitCt noise rules (:160-176).  The first round's SubBytes + ShiftRows run; MixColumns raises."""
+    ck, ctx = keys
+    g = golden["test_light"]
+    key = bytes.fromhex(g["key"])
+    blk = bytes.fromhex(golden["chacha20_zero_seed"]["block1"])
+    ek = aes_128.encrypt_word_array(ck, aes_128.key_schedule_plain(key))
+    block = aes_128.encrypt_byte_array(ck, blk)
+    enc = aes_128.ShortintWoppbs1BitSboxPbsAesEncrypt
+    out = enc.encrypt_block_for_rounds(ctx, ek, block, 1)  # no MixColumns in a 1-round run
+    assert aes_128.decrypt_byte_array(ck, out).hex() == g["block1"]["1"]
+    with pytest.raises((tfhe_aes.NoiseNotIndependent, tfhe_aes.NoiseTooBig)):
+        enc.encrypt_block_for_rounds(ctx, ek, block, 2)

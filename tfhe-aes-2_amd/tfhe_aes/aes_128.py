@@ -213,6 +213,75 @@ class ShortintWoppbs8BitSboxPbsAesEncrypt(ShortintWoppbs1BitSboxGalMulPbsAesEncr
     """
 
 
+class ShortintWoppbs1BitSboxPbsAesEncrypt:
+    """fhe_impls/shortint_woppbs_1bit.rs:47-81: the generic fhe_sbox_pbs driver (fhe_sbox_pbs.rs:22-121)
+    over the 1-bit model -- SubBytes = Byte::sbox_substitute (one 8 -> 8 circuit bootstrap per byte),
+    MixColumns = gf_256_mul by BitCt XORs (:33-73), AddRoundKey / ShiftRows as data_model.rs:270-281.
+
+    The reference ships this combination with its tests #[ignore]d ("does not work since cipher text
+    noise is not independent in calculations", fhe_impls/shortint_woppbs_1bit.rs:160-176): the leveled
+    MixColumns trips the BitCt noise bookkeeping, which raises here exactly as it panics there
+    (NoiseNotIndependent / NoiseTooBig from tae_bit_xor_assign).  Host-driven, one byte per call.
+    """
+
+    @staticmethod
+    def _xor(a: List[BitCt], b: List[BitCt]) -> List[BitCt]:
+        out = [x.clone() for x in a]
+        for x, y in zip(out, b):
+            x ^= y
+        return out
+
+    @staticmethod
+    def _gf_256_mul(ctx: FheContext, a: List[BitCt], b: int) -> List[BitCt]:
+        a = [x.clone() for x in a]
+        res = [ctx.trivial(Cleartext(0)) for _ in range(8)]
+        for _ in range(8):
+            if b & 1:
+                for x, y in zip(res, a):
+                    x ^= y
+            reduce_x8 = a[0]  # Byte::shl_assign_1 (data_model.rs:45-49)
+            a = a[1:] + [ctx.trivial(Cleartext(0))]
+            for i in (3, 4, 6, 7):
+                a[i] ^= reduce_x8
+            b >>= 1
+        return res
+
+    @staticmethod
+    def encrypt_block_for_rounds(ctx: FheContext, expanded_key, block, rounds: int):
+        """expanded_key: [44][4][8] BitCt; block: [16][8] BitCt (byte 4 c + r = state[r][c])."""
+        cls = ShortintWoppbs1BitSboxPbsAesEncrypt
+        lut = ctx.generate_lookup_table(8, 8, lambda v: SBOX[v])
+        state = [[list(block[4 * c + r]) for c in range(4)] for r in range(4)]  # State::from_array
+
+        def xor_state(words):
+            for c in range(4):
+                for r in range(4):
+                    state[r][c] = cls._xor(state[r][c], words[c][r])
+
+        def sub_bytes_shift_rows():
+            for r in range(4):
+                row = [ctx.circuit_bootstrap(state[r][c], lut) for c in range(4)]
+                state[r] = row[r:] + row[:r]
+
+        xor_state(expanded_key[0:4])
+        for i in range(1, rounds):
+            sub_bytes_shift_rows()
+            cols = []
+            for c in range(4):  # mix_columns
+                col = [state[r][c] for r in range(4)]
+                cols.append([cls._xor(cls._xor(cls._xor(cls._gf_256_mul(ctx, col[r], 2),
+                                                        cls._gf_256_mul(ctx, col[(r - 1) % 4], 1)),
+                                               cls._gf_256_mul(ctx, col[(r - 2) % 4], 1)),
+                                      cls._gf_256_mul(ctx, col[(r - 3) % 4], 3)) for r in range(4)])
+            for c in range(4):
+                for r in range(4):
+                    state[r][c] = cols[c][r]
+            xor_state(expanded_key[4 * i:4 * i + 4])
+        sub_bytes_shift_rows()
+        xor_state(expanded_key[40:44])
+        return [state[i % 4][i // 4] for i in range(16)]  # State::into_array
+
+
 def counter_blocks(iv: bytes, count: int) -> List[bytes]:
     """main.rs:108-115: block = iv (8 bytes) || ctr as u64 big-endian, ctr = 1..=count."""
     return [bytes(iv) + c.to_bytes(8, "big") for c in range(1, count + 1)]
