@@ -459,20 +459,26 @@ __global__ void __launch_bounds__(512, 1)
         const int cur = ks & 1;
         if (ks + 1 < nk) gload((ks + 1) * TK);
 #pragma unroll
-        for (int kk = 0; kk < TK / 32; kk++) {
-            if (kk == TK / 64 && ks + 1 < nk) lstore(cur ^ 1);
-            v4i fa[3], fb[2];
+        // fragments of step kk + 1 are read from LDS while the MFMAs of step kk run
+        v4i fa[2][3], fb[2][2];
+        auto ldfrag = [&](int kk, v4i *xa, v4i *xb) {
 #pragma unroll
             for (int m = 0; m < 3; m++)
-                fa[m] = *reinterpret_cast<const v4i *>(&sA(cur)[(wm * 96 + m * 32 + r) * LROW + kk * 32 + h * 16]);
+                xa[m] = *reinterpret_cast<const v4i *>(&sA(cur)[(wm * 96 + m * 32 + r) * LROW + kk * 32 + h * 16]);
 #pragma unroll
             for (int tj = 0; tj < 2; tj++)
-                fb[tj] = *reinterpret_cast<const v4i *>(&sB(cur)[(wn * 64 + tj * 32 + r) * LROW + kk * 32 + h * 16]);
+                xb[tj] = *reinterpret_cast<const v4i *>(&sB(cur)[(wn * 64 + tj * 32 + r) * LROW + kk * 32 + h * 16]);
+        };
+        ldfrag(0, fa[0], fb[0]);
+#pragma unroll
+        for (int kk = 0; kk < TK / 32; kk++) {
+            if (kk == TK / 64 && ks + 1 < nk) lstore(cur ^ 1);
+            if (kk + 1 < TK / 32) ldfrag(kk + 1, fa[(kk + 1) & 1], fb[(kk + 1) & 1]);
 #pragma unroll
             for (int m = 0; m < 3; m++)
 #pragma unroll
                 for (int tj = 0; tj < 2; tj++)
-                    acc[m][tj] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[m], fb[tj], acc[m][tj], 0, 0, 0);
+                    acc[m][tj] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[kk & 1][m], fb[kk & 1][tj], acc[m][tj], 0, 0, 0);
         }
         if (ks + 1 < nk) __syncthreads();
     }
