@@ -458,7 +458,6 @@ __global__ void __launch_bounds__(512, 1)
     for (int ks = 0; ks < nk; ks++) {
         const int cur = ks & 1;
         if (ks + 1 < nk) gload((ks + 1) * TK);
-#pragma unroll
         // fragments of step kk + 1 are read from LDS while the MFMAs of step kk run
         v4i fa[2][3], fb[2][2];
         auto ldfrag = [&](int kk, v4i *xa, v4i *xb) {
