@@ -58,6 +58,9 @@ def main():
     ap.add_argument("--key-schedule", choices=["fhe", "plain"], default="fhe")
     ap.add_argument("--cpu-baseline", choices=["auto", "on", "off"], default="auto")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--single-block", choices=["auto", "on", "off"], default="auto",
+                    help="also time one block alone (BASELINE configs[1]: 16 SBOX x 10 rounds on 1 GPU); "
+                         "auto = on at world size 1")
     ap.add_argument("--model", choices=["1bit", "8bit"], default="1bit",
                     help="1bit: ShortintWoppbs1BitSboxGalMulPbsAesEncrypt (params_sqrd_lvl_64, the metric); "
                          "8bit: ShortintWoppbs8BitSboxPbsAesEncrypt (BASELINE config #5)")
@@ -172,6 +175,27 @@ def main():
     if not ok:
         raise SystemExit(f"rank {rank}: decrypted AES output differs from plain AES")
 
+    # ---- BASELINE configs[1]: one block alone (latency; not the headline value) ----
+    single = None
+    if args.single_block == "on" or (args.single_block == "auto" and world == 1):
+        one_dev = blk_dev[:128].contiguous()
+        one_out = torch.empty_like(one_dev)
+
+        def one():
+            E.encrypt_blocks_device(ctx, rk_dev.data_ptr(), one_dev.data_ptr(), 1, args.rounds, one_out.data_ptr())
+        one()
+        ctx.synchronize()
+        reps, t1 = 3, time.time()
+        for _ in range(reps):
+            one()
+        ctx.synchronize()
+        lat = (time.time() - t1) / reps
+        got1 = aes_128.bits_to_blocks(ck.decrypt_bits_raw(one_out.cpu().numpy().view(np.uint64)))[0]
+        single = {"config": "1 block, 16 SBOX x %d rounds on 1 GPU" % args.rounds, "s_per_block": lat,
+                  "blocks_per_s": 1.0 / lat, "per_sbox_ms": lat * 1e3 / (16 * args.rounds),
+                  "correct": got1 == aes_128.encrypt_block_plain(aes_128.key_schedule_plain(README_KEY), blocks[0],
+                                                                 args.rounds)}
+
     total_blocks = nb * world * args.steps
     value = total_blocks / elapsed
     ms_per_step = elapsed * 1000.0 / args.steps
@@ -224,7 +248,7 @@ def main():
                "roofline": roofline, "cpu_baseline": cpu,
                "stage_ms_per_step": stage_share, "per_sbox_ms": ms_per_step / (nb * 16 * args.rounds),
                "keygen_s": keygen_s, "key_setup_s": key_setup_s, "key_expansion_s": key_expansion_s,
-               "encrypt_s": encrypt_s, "correct": bool(ok)}
+               "encrypt_s": encrypt_s, "correct": bool(ok), "single_block": single}
         print(json.dumps(rec), flush=True)
     if dist:
         dist.destroy_process_group()
