@@ -70,6 +70,22 @@ def test_pbs_shift_boolean_bit_exact(gpu_context, oracle_keys, bits_cts):
         assert min(err, (1 << 64) - err) < 1 << 45
 
 
+@pytest.mark.parametrize("kernel", ["br512lat", "br512x4"])
+def test_pbs_kernels_bit_exact(product_raw, oracle_keys, bits_cts, kernel, monkeypatch):
+    """Both N=512 blind rotations on the same 7 ciphertexts: the small-batch latency kernel (one
+    ciphertext per workgroup, levels in parallel) and the throughput kernel (three per workgroup,
+    forced with TAE_BR_LAT_MAX=0), each equal to the oracle word for word."""
+    monkeypatch.setenv("TAE_BR_LAT_MAX", "256" if kernel == "br512lat" else "0")
+    ctx = tfhe_aes.context_from_raw(tfhe_aes.PARAMS_SQRD_LVL_64, product_raw[1], device=0)
+    bits, cts = bits_cts
+    n = 7
+    small = np.stack([oracle_keys.keyswitch(cts[i]) for i in range(n)])
+    out = np.zeros((n, BIG), dtype=np.uint64)
+    _stage(N.lib().tae_stage_pbs_shift_boolean, ctx._h, _vp(small), n, 1, _vp(out), N.TAE_MEM_HOST)
+    for i in range(n):
+        assert np.array_equal(out[i], oracle_keys.homomorphic_shift_boolean(small[i], 1)), i
+
+
 def test_pfks_bit_exact(gpu_context, oracle_keys, bits_cts):
     bits, cts = bits_cts
     n = 2

@@ -21,6 +21,7 @@
 #include "br512x2.hpp"
 #include "br512x4.hpp"
 #include "br512x5.hpp"
+#include "br512lat.hpp"
 #include "br1024.hpp"
 #include "ksgemm.hpp"
 #include "engine.hpp"
@@ -640,7 +641,14 @@ void Engine::init_common() {
     // than the 128 VGPRs of 4 waves per SIMD and spills (295 ms vs 205 ms per PBS launch)
     const char *bx5 = getenv("TAE_BR_X5");
     x5_512_ = x4_512_ && bx5 && bx5[0] == '1';
+    // small batches: one ciphertext per workgroup, levels in parallel (br512lat.hpp); TAE_BR_LAT_MAX
+    // overrides the batch-size threshold (0 disables)
+    const char *blat = getenv("TAE_BR_LAT_MAX");
+    lat512_ = x4_512_;
+    lat_max_ = blat ? atol(blat) : 256;
     if (batched512_) {
+        HIPC(hipFuncSetAttribute((const void *)br512lat::br_kernel<3, 12>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)br512lat::lds_bytes(3)));
         HIPC(hipFuncSetAttribute((const void *)br512x5::br_kernel<3, true, 12>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         HIPC(hipFuncSetAttribute((const void *)br512x5::br_kernel<1, false, 13>,
@@ -817,6 +825,12 @@ void Engine::bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint
     if (batched512_ && p_.pbs_l == 3) {
         const br512::W16 W = make_w16(w16_);
         const size_t wgs = (B + kBrC - 1) / kBrC;
+        if (lat512_ && (long)B <= lat_max_) {
+            br512lat::br_kernel<3, 12><<<(unsigned)B, br512lat::THREADS, br512lat::lds_bytes(3), stream_>>>(
+                d_small, p_.n, d_lut_glwe, d_bsk_f_, d_big, (long)B, body_add, out_add, d_twist_, d_w_);
+            HIPC(hipGetLastError());
+            return;
+        }
         if (x5_512_) {
             br512x5::br_kernel<3, true, 12><<<(unsigned)wgs, br512x5::THREADS, br512x5::lds_bytes(), stream_>>>(
                 d_small, p_.n, d_lut_glwe, 0, d_bsk_f_, 0, d_big, (long)B, body_add, out_add, d_twist_, d_w_);
