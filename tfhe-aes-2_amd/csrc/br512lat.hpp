@@ -2,9 +2,10 @@
 // ONE ciphertext per 1024-thread workgroup, and the decomposition LEVELS run in parallel instead
 // of one after another.  Wave jb < LEV * (k+1) owns FFT job (level jb / (k+1) + 1, polynomial
 // jb % (k+1)), so a CMux step is
-//   decomposition + forward FFT of all LEV * (k+1) digit polynomials   (one wave each) | barrier
+//   forward FFT of all LEV * (k+1) digit polynomials                    (one wave each) | barrier
 //   MAC of all levels: thread task (q, position) = 15 complex terms     -> out[q]       | barrier
-//   inverse FFT of the k+1 outputs (waves 0..k), ACC +=                                  | barrier
+//   inverse FFT of the k+1 outputs (waves 0..k), ACC +=, and the next step's decomposition of
+//   that polynomial (all levels once; the finer levels to LDS for their FFT waves)       | barrier
 // three barriers per step instead of the 2 LEV + 1 of br512x4 (which spends them on three
 // ciphertexts per workgroup for throughput).  The FFT jobs reuse br512x4's 4-lane DFT16
 // (dft16x4), and every output keeps the oracle's operation order (levels descending, rows
@@ -33,6 +34,23 @@ using br512x4::dft16x4;
 
 constexpr int THREADS = 1024;
 
+// TAE_LAT_PROF (debug builds only): per-phase cycle sums of every wave of workgroup 0
+#ifdef TAE_LAT_PROF
+#define LPROF_DECL uint64_t lprof_[8] = {0}, lprof_t_ = clock64();
+#define LPROF(i)                           \
+    do {                                   \
+        asm volatile("" ::: "memory");     \
+        const uint64_t now_ = clock64();   \
+        lprof_[i] += now_ - lprof_t_;      \
+        lprof_t_ = now_;                   \
+    } while (0)
+#else
+#define LPROF_DECL
+#define LPROF(i) \
+    do {         \
+    } while (0)
+#endif
+
 template <int LEV, int BLOG>
 __global__ void __launch_bounds__(THREADS, 1)
     br_kernel(const uint64_t *__restrict__ lwe_in, int n, const uint64_t *__restrict__ lut,
@@ -48,6 +66,7 @@ __global__ void __launch_bounds__(THREADS, 1)
     cplx *s_twa = s_tw + M;                                         // [16 a + b] = W_M^{a b}
     cplx *s_utw = s_twa + M;                                        // conj(twist) 2^-8 (exact)
     cplx *s_w16 = s_utw + M;                                        // [r][3]: W16^{r k1}
+    uint32_t *s_dig = reinterpret_cast<uint32_t *>(s_w16 + 12);     // [LEV-1][K1][4][64] digits
     const long ct = blockIdx.x;
     if (ct >= B) return;  // whole workgroup
     const int tid = threadIdx.x;
@@ -121,8 +140,35 @@ __global__ void __launch_bounds__(THREADS, 1)
     uint32_t pf_prev[PF], pf_cur[PF];
 #pragma unroll
     for (int i = 0; i < PF; i++) pf_prev[i] = 0;
+    // Decomposition of polynomial jb (waves 0..k, the level-1 jobs, which also own output q = jb of
+    // the inverse FFT and so update ACC polynomial jb): all levels at once, once per polynomial;
+    // level 1 stays in registers, the finer levels go to LDS for the waves of those jobs.
+    uint32_t mydig[4];
+    auto decompose_poly = [&](int e) {
+        const uint64_t *poly = acc + jb * N;
+        const int bt = ll - e;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int j = ll + 64 * i;
+            const int t = (bt + 64 * i) & (2 * N - 1);
+            const int ph = t & (N - 1);
+            const uint64_t m0 = (uint64_t)(int64_t)((t << 22) >> 31);
+            const uint64_t m1 = (uint64_t)(int64_t)(((t + M) << 22) >> 31);
+            const uint64_t v0 = poly[ph], v1 = poly[ph ^ M];
+            const uint64_t p0 = poly[j], p1 = poly[j + M];
+            const uint64_t x0 = (v0 ^ m0) - (p0 + m0), x1 = (v1 ^ m1) - (p1 + m1);
+            uint32_t d0[LEV], d1[LEV];
+            decompose16<LEV>(x0, BLOG, d0);
+            decompose16<LEV>(x1, BLOG, d1);
+            mydig[i] = d0[0] | (d1[0] << 16);
+#pragma unroll
+            for (int l = 1; l < LEV; l++) s_dig[(((l - 1) * K1 + jb) * 4 + i) * 64 + ll] = d0[l] | (d1[l] << 16);
+        }
+    };
+    if (jb < K1 && n > 0) decompose_poly(mod_switch(in[0], LOGN) % (2 * N));
+    lds_sync();
+    LPROF_DECL
     for (int step = 0; step < n; step++) {
-        const int e = mod_switch(in[step], LOGN) % (2 * N);
         const int gstep = step * (int)(ggsw_sz * sizeof(cplx));
 #ifndef TAE_LAT_NOPF
         if (step + 2 < n) {
@@ -141,29 +187,15 @@ __global__ void __launch_bounds__(THREADS, 1)
         }
 #endif
         if (fjob) {
-            // rotated difference + the job's level of the decomposition, coefficients j = ll + 64 i (+ M)
-            const uint64_t *poly = acc + jp * N;
-            const int bt = ll - e;
             uint32_t dig[4];
+            if (jb < K1) {  // level 1: computed by this wave at the end of the previous step
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const int j = ll + 64 * i;
-                const int t = (bt + 64 * i) & (2 * N - 1);
-                const int ph = t & (N - 1);
-                const uint64_t m0 = (uint64_t)(int64_t)((t << 22) >> 31);
-                const uint64_t m1 = (uint64_t)(int64_t)(((t + M) << 22) >> 31);
-                const uint64_t v0 = poly[ph], v1 = poly[ph ^ M];
-                const uint64_t p0 = poly[j], p1 = poly[j + M];
-                const uint64_t x0 = (v0 ^ m0) - (p0 + m0), x1 = (v1 ^ m1) - (p1 + m1);
-                uint32_t d0[LEV], d1[LEV];
-                decompose16<LEV>(x0, BLOG, d0);
-                decompose16<LEV>(x1, BLOG, d1);
-                uint32_t dw = d0[0] | (d1[0] << 16);
+                for (int i = 0; i < 4; i++) dig[i] = mydig[i];
+            } else {
 #pragma unroll
-                for (int l = 1; l < LEV; l++)
-                    if (jlev - 1 == l) dw = d0[l] | (d1[l] << 16);
-                dig[i] = dw;
+                for (int i = 0; i < 4; i++) dig[i] = s_dig[(((jlev - 2) * K1 + jp) * 4 + i) * 64 + ll];
             }
+            LPROF(0);
             // pass A (column u): twist, DFT16 over m = r + 4 i, W_M^{u k} -> position u + 16 k
             cplx *dst = buf + jb * BUF_STRIDE;
             cplx v[4];
@@ -180,6 +212,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                 dst[pidx(u + 16 * kq)] = cmul(v[k2], s_twa[16 * kq + u]);
             }
             wave_sync();
+            LPROF(1);
             // pass B (row u): DFT16 over positions 16 u + r + 4 i, in place
 #pragma unroll
             for (int i = 0; i < 4; i++) v[i] = dst[pidx(16 * u + r + 4 * i)];
@@ -187,10 +220,14 @@ __global__ void __launch_bounds__(THREADS, 1)
 #pragma unroll
             for (int k2 = 0; k2 < 4; k2++) dst[pidx(16 * u + r + 4 * k2)] = v[k2];
         }
+        LPROF(2);
         lds_sync();
+        LPROF(3);
         mac_task(q0, pos0, gstep);
         if (tid >= 3 * M) mac_task(K1 - 1, pos0, gstep);
+        LPROF(4);
         lds_sync();
+        LPROF(5);
         if (jb < K1) {  // inverse FFT of output q = jb, ACC +=
             cplx *base = obuf + jb * BUF_STRIDE;
             cplx v[4];
@@ -214,9 +251,20 @@ __global__ void __launch_bounds__(THREADS, 1)
                 poly[j] += from_torus_bits(t.re);
                 poly[j + M] += from_torus_bits(t.im);
             }
+            wave_sync();
+            if (step + 1 < n) decompose_poly(mod_switch(in[step + 1], LOGN) % (2 * N));
         }
+        LPROF(6);
         lds_sync();
+        LPROF(7);
     }
+#ifdef TAE_LAT_PROF
+    if (blockIdx.x == 0 && lane == 0)
+        printf("latprof wave %2d: dec %llu passA %llu passB %llu bar1 %llu mac %llu bar2 %llu inv %llu bar3 %llu\n", jb,
+               (unsigned long long)lprof_[0], (unsigned long long)lprof_[1], (unsigned long long)lprof_[2],
+               (unsigned long long)lprof_[3], (unsigned long long)lprof_[4], (unsigned long long)lprof_[5],
+               (unsigned long long)lprof_[6], (unsigned long long)lprof_[7]);
+#endif
     uint64_t *o = out + (size_t)ct * ((K1 - 1) * N + 1);
     for (int t = tid; t < (K1 - 1) * N; t += THREADS) {
         const int p = t / N, j = t - p * N;
@@ -226,7 +274,8 @@ __global__ void __launch_bounds__(THREADS, 1)
 }
 
 inline size_t lds_bytes(int lev) {
-    return (size_t)K1 * N * 8 + (size_t)(lev * K1 + K1) * BUF_STRIDE * 16 + 3 * (size_t)M * 16 + 12 * 16;
+    return (size_t)K1 * N * 8 + (size_t)(lev * K1 + K1) * BUF_STRIDE * 16 + 3 * (size_t)M * 16 + 12 * 16 +
+           (size_t)(lev - 1) * K1 * 4 * 64 * 4;
 }
 
 }  // namespace br512lat
