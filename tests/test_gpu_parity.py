@@ -86,6 +86,20 @@ def test_pbs_kernels_bit_exact(product_raw, oracle_keys, bits_cts, kernel, monke
         assert np.array_equal(out[i], oracle_keys.homomorphic_shift_boolean(small[i], 1)), i
 
 
+def test_pbs_split_batch_bit_exact(gpu_context, oracle_keys, client):
+    """A batch of 3 x 256 + 5 ciphertexts: whole rounds on br512x4, the 5-ciphertext remainder on
+    br512lat (Engine::bootstrap); ciphertexts from both parts equal the oracle's."""
+    B = 3 * 256 + 5
+    bits = np.random.default_rng(7).integers(0, 2, size=B).astype(np.uint8)
+    cts = client.encrypt_bits_raw(bits, start_index=40_000)
+    small = np.zeros((B, SMALL), dtype=np.uint64)
+    _stage(N.lib().tae_stage_keyswitch, gpu_context._h, _vp(cts), B, _vp(small), N.TAE_MEM_HOST)
+    out = np.zeros((B, BIG), dtype=np.uint64)
+    _stage(N.lib().tae_stage_pbs_shift_boolean, gpu_context._h, _vp(small), B, 1, _vp(out), N.TAE_MEM_HOST)
+    for i in (0, 767, 768, B - 1):
+        assert np.array_equal(out[i], oracle_keys.homomorphic_shift_boolean(small[i], 1)), i
+
+
 def test_pfks_bit_exact(gpu_context, oracle_keys, bits_cts):
     bits, cts = bits_cts
     n = 2

@@ -165,6 +165,7 @@ class Engine {
     bool x4_512_ = false;     // ... as 1024-thread workgroups (br512x4.hpp; TAE_BR_X2=1 -> br512x2.hpp)
     bool lat512_ = false;     // small batches on br512lat.hpp (B <= lat_max_)
     long lat_max_ = 256;
+    int num_cu_ = 256;
     bool x5_512_ = false;     // ... with ACC in registers, double-buffered spectra (br512x5.hpp; opt-in TAE_BR_X5=1)
     bool wide512_ = false;    // ... as 512-thread workgroups (br512x2.hpp; TAE_BR_256=1 -> br512.hpp)
     bool timing_ = false;

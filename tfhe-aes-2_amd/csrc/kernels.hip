@@ -646,6 +646,7 @@ void Engine::init_common() {
     const char *blat = getenv("TAE_BR_LAT_MAX");
     lat512_ = x4_512_;
     lat_max_ = blat ? atol(blat) : 256;
+    HIPC(hipDeviceGetAttribute(&num_cu_, hipDeviceAttributeMultiprocessorCount, device_));
     if (batched512_) {
         HIPC(hipFuncSetAttribute((const void *)br512lat::br_kernel<3, 12>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)br512lat::lds_bytes(3)));
@@ -838,9 +839,21 @@ void Engine::bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint
             return;
         }
         if (x4_512_) {
-            br512x4::br_kernel<3, true, 12><<<(unsigned)wgs, br512x4::THREADS, br512x4::lds_bytes(), stream_>>>(
-                d_small, p_.n, d_lut_glwe, 0, d_bsk_f_, 0, d_big, (long)B, body_add, out_add, d_twist_, d_w_);
+            // whole rounds of three ciphertexts per CU on br512x4; a remainder that would leave most
+            // CUs idle in a last round goes to br512lat (one ciphertext per CU, ~0.6x the round time)
+            long bx = (long)B;
+            const long per_round = 3L * num_cu_, rest = (long)B % per_round;
+            if (lat512_ && (long)B > per_round && rest > 0 && rest <= std::min<long>(lat_max_, num_cu_)) bx -= rest;
+            br512x4::br_kernel<3, true, 12><<<(unsigned)((bx + 2) / 3), br512x4::THREADS, br512x4::lds_bytes(),
+                                               stream_>>>(d_small, p_.n, d_lut_glwe, 0, d_bsk_f_, 0, d_big, bx,
+                                                          body_add, out_add, d_twist_, d_w_);
             HIPC(hipGetLastError());
+            if (bx < (long)B) {
+                br512lat::br_kernel<3, 12><<<(unsigned)(B - bx), br512lat::THREADS, br512lat::lds_bytes(3), stream_>>>(
+                    d_small + (size_t)bx * (p_.n + 1), p_.n, d_lut_glwe, d_bsk_f_, d_big + (size_t)bx * p_.big_len(),
+                    (long)B - bx, body_add, out_add, d_twist_, d_w_);
+                HIPC(hipGetLastError());
+            }
             return;
         }
         if (wide512_) {
