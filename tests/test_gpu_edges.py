@@ -1,0 +1,76 @@
+"""Edge cases of the batched device path: empty and ragged batches, argument errors.
+
+Ragged: the blind rotations pack 3 ciphertexts (PBS / vertical packing, br512x4) or 1 (br512lat)
+per workgroup, so output counts that are not multiples of 3 and single-group batches exercise the
+partial workgroups; every output is compared with the oracle or decrypted.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import tfhe_aes
+from tfhe_aes import _native as N
+from tfhe_aes import aes_128
+
+pytestmark = pytest.mark.gpu
+
+BIG = 4 * 512 + 1
+
+
+def _vp(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+@pytest.fixture(scope="module")
+def client(product_raw):
+    return product_raw[0]
+
+
+def test_empty_batches(gpu_context, client):
+    lut = gpu_context.generate_lookup_table(8, 8, lambda v: aes_128.SBOX[v])
+    out = gpu_context.circuit_bootstrap_raw(np.zeros((0, 8, BIG), dtype=np.uint64), lut)
+    assert out.shape == (0, 8, BIG)
+    rk = client.encrypt_bits_raw([0] * 1408, start_index=1 << 30)
+    blocks = np.zeros((0, 128, BIG), dtype=np.uint64)
+    out = aes_128.ShortintWoppbs1BitSboxGalMulPbsAesEncrypt.encrypt_blocks_raw(gpu_context, rk, blocks, 2)
+    assert out.shape == (0, 128, BIG)
+    z = np.zeros((1, BIG), dtype=np.uint64)
+    N.check(N.lib().tae_stage_keyswitch(gpu_context._h, _vp(z), 0, _vp(z), N.TAE_MEM_HOST))
+    N.check(N.lib().tae_stage_pbs_shift_boolean(gpu_context._h, _vp(z), 0, 1, _vp(z), N.TAE_MEM_HOST))
+
+
+@pytest.mark.parametrize("n_out", [1, 5, 24])
+def test_ragged_outputs_bit_exact(gpu_context, oracle_keys, client, n_out):
+    """8 -> n_out LUTs (vertical packing with n_out % 3 != 0 and the 24-output galois LUT), two groups."""
+    f = lambda v: (aes_128.SBOX[v] * 0x10101 ^ v) & ((1 << n_out) - 1)
+    lut = gpu_context.generate_lookup_table(8, n_out, f)
+    vals = [0x3C, 0xA7]
+    bits = np.stack([client.encrypt_bits_raw(aes_128.u8_to_bits(v), start_index=80_000 + 8 * i + 100 * n_out)
+                     for i, v in enumerate(vals)])
+    out = gpu_context.circuit_bootstrap_raw(bits, lut)
+    for g, v in enumerate(vals):
+        got = [int(b) for b in client.decrypt_bits_raw(out[g])]
+        assert got == [(f(v) >> (n_out - 1 - j)) & 1 for j in range(n_out)], (g, hex(v))
+    assert np.array_equal(out[1], oracle_keys.circuit_bootstrap(bits[1], lut.as_array(), n_out))
+
+
+def test_argument_errors(gpu_context, client):
+    lut = gpu_context.generate_lookup_table(8, 8, lambda v: v)
+    bits = np.zeros((1, 7, BIG), dtype=np.uint64)
+    with pytest.raises(tfhe_aes.TaeError) as e:
+        gpu_context.circuit_bootstrap_raw(bits, lut)  # 7 bits for an 8-input LUT
+    assert e.value.code == N.TAE_E_ARG
+    z = np.zeros((2, BIG), dtype=np.uint64)
+    for level in (0, 2):  # params_sqrd_lvl_64 has cbs_l = 1
+        with pytest.raises(tfhe_aes.TaeError):
+            N.check(N.lib().tae_stage_pbs_shift_boolean(gpu_context._h, _vp(z), 1, level, _vp(z), N.TAE_MEM_HOST))
+    rk = client.encrypt_bits_raw([0] * 1408, start_index=1 << 31)
+    blocks = client.encrypt_bits_raw([0] * 128, start_index=(1 << 31) + 4096).reshape(1, 128, BIG)
+    for rounds in (0, 11):
+        with pytest.raises(tfhe_aes.TaeError) as e:
+            aes_128.ShortintWoppbs1BitSboxGalMulPbsAesEncrypt.encrypt_blocks_raw(gpu_context, rk, blocks, rounds)
+        assert e.value.code == N.TAE_E_PARAM
+    with pytest.raises(tfhe_aes.TaeError) as e:
+        tfhe_aes.get_params(99)
+    assert e.value.code == N.TAE_E_PARAM
