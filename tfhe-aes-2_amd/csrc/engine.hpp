@@ -150,6 +150,7 @@ class Engine {
     void collect_times();
     // int8 MFMA keyswitches (ksgemm.hpp): key limb matrices + digit scratch
     bool mfma_ks_ = false;
+    bool glds_gemm_ = true;   // PFKS on the LDS-DMA GEMM (ksgemm.hpp gemm_g4; TAE_GEMM_GLDS=0: gemm_big3)
     bool gemm3_ = true;     // PFKS digits as 3 x 6-bit limbs (TAE_GEMM_MA4=1: 4 x 5 bits)
     bool big_gemm_ = true;  // PFKS on the 256 x 256-tile GEMM (TAE_GEMM_SMALL=1: 128 x 128)
     int8_t *d_pf_bt_ = nullptr, *d_ks_bt_ = nullptr, *d_digits_ = nullptr;

@@ -729,6 +729,10 @@ void Engine::prepare_mfma_keys() {
                              (int)ksgemm::gemm_big_lds()));
     HIPC(hipFuncSetAttribute((const void *)ksgemm::gemm_big3<6>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)ksgemm::gemm_big3_lds()));
+    HIPC(hipFuncSetAttribute((const void *)ksgemm::gemm_g4<6>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)ksgemm::gemm_g4_lds()));
+    const char *gl = getenv("TAE_GEMM_GLDS");
+    glds_gemm_ = !(gl && gl[0] == '0');  // TAE_GEMM_GLDS=0: register-staged gemm_big3
     const char *v = getenv("TAE_KS_VALU");
     mfma_ks_ = !(v && v[0] == '1') && p_.pfks_b * 1 <= 16 && p_.ks_b <= 7;
     if (!mfma_ks_) return;
@@ -908,8 +912,12 @@ void Engine::pfks_into_ggsw(const uint64_t *d_big, uint64_t *d_ggsw, size_t B, i
         const int ncols = (p_.k + 1) * glwe;
         const long out_stride = (long)p_.cbs_l * ncols;
         const long ntiles = ((long)ncols * 8 + ksgemm::BTN - 1) / ksgemm::BTN;
-        ksgemm::gemm_big3<6><<<(unsigned)(mtiles * ntiles), 512, ksgemm::gemm_big3_lds(), stream_>>>(
-            d_digits_, d_pf_bt_, kp_pf_, mtiles, ncols, d_ggsw + (size_t)(level - 1) * ncols, out_stride, (long)B);
+        if (glds_gemm_ && kp_pf_ % ksgemm::G4K == 0)
+            ksgemm::gemm_g4<6><<<(unsigned)(mtiles * ntiles), 512, ksgemm::gemm_g4_lds(), stream_>>>(
+                d_digits_, d_pf_bt_, kp_pf_, mtiles, ncols, d_ggsw + (size_t)(level - 1) * ncols, out_stride, (long)B);
+        else
+            ksgemm::gemm_big3<6><<<(unsigned)(mtiles * ntiles), 512, ksgemm::gemm_big3_lds(), stream_>>>(
+                d_digits_, d_pf_bt_, kp_pf_, mtiles, ncols, d_ggsw + (size_t)(level - 1) * ncols, out_stride, (long)B);
         HIPC(hipGetLastError());
         return;
     }

@@ -511,5 +511,150 @@ __global__ void __launch_bounds__(512, 1)
 
 inline size_t gemm_big3_lds() { return (size_t)2 * (B3M + BTN) * LROW; }
 
+// ---- gemm_big3 with LDS-DMA staging: global_load_lds (16 B per lane, no VGPR staging, no
+// ds_write) into a 4-stage ring of 64-byte K steps, two steps kept in flight across the per-step
+// barrier by a counted vmcnt (cdna_hip_programming.md section 5: "Async global->LDS copy",
+// "Pipelining across barriers").  The LDS image is lane-linear (rows of 64 B, no padding), so the
+// bank-conflict swizzle (16-byte chunk c of row r stored at c ^ ((r >> 2) & 3)) goes on the
+// per-lane global source address and on the fragment reads.  Same tiles, limbs and epilogue as
+// gemm_big3: bit-identical results. ----
+constexpr int G4K = 64, G4S = 4;                      // K bytes per step, ring stages
+constexpr int G4A = B3M * G4K, G4B = BTN * G4K;       // bytes per stage
+__device__ __forceinline__ int g4_swz(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
+
+// global_load_lds_dwordx4: 16 bytes per lane from src to lds_base + 16 * lane (lds_base wave-uniform).
+// The target builtin exists only in the device pass of the single-source compile.
+__device__ __forceinline__ void g4_glds(const int8_t *src, int8_t *lds_base) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_global_load_lds(src, lds_base, 16, 0, 0);
+#else
+    (void)src;
+    (void)lds_base;
+#endif
+}
+
+template <int LB3>
+__global__ void __launch_bounds__(512, 1)
+    gemm_g4(const int8_t *__restrict__ A, const int8_t *__restrict__ Bt, int Kp, long mtiles, int ncols,
+            uint64_t *__restrict__ out, long out_stride, long B) {
+    extern __shared__ __align__(16) int8_t smem_g[];
+    const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int wm = wave >> 2, wn = wave & 3;
+    constexpr long GN = 16;
+    const long ntiles = (((long)ncols * 8) + BTN - 1) / BTN;
+    const long gsz = GN * mtiles;
+    const long ng = blockIdx.x / gsz, rr = blockIdx.x - ng * gsz;
+    const long gw = min(GN, ntiles - ng * GN);
+    const long mt = rr / gw, nt = ng * GN + (rr - (rr / gw) * gw);
+    const long row0 = mt * B3M;
+    const long col8_0 = nt * BTN;
+    const long N8 = (long)ncols * 8;
+    auto sA = [&](int st) { return smem_g + st * (G4A + G4B); };
+    auto sB = [&](int st) { return smem_g + st * (G4A + G4B) + G4A; };
+
+    // one glds wave-instruction = 16 rows x 4 chunks (1 KiB).  Per stage: A 12 of them (waves 0-5
+    // issue 2), B 16 (every wave 2) -> 4 or 2 per wave
+    const int lrow = lane >> 2, lch = lane & 3;
+    auto stage = [&](int st, int ks) {
+        const int k0 = ks * G4K;
+        if (wave < 6) {
+#pragma unroll
+            for (int t = 0; t < 2; t++) {
+                const int r16 = (wave * 2 + t) * 16;  // first row of this piece
+                const int row = r16 + lrow;
+                const int8_t *src = A + (row0 + row) * Kp + k0 + 16 * g4_swz(row, lch);
+                g4_glds(src, sA(st) + r16 * G4K);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+            const int r16 = (wave * 2 + t) * 16;
+            const int row = r16 + lrow;
+            const long br = min(col8_0 + row, N8 - 1);  // rows past the last column feed unstored outputs
+            const int8_t *src = Bt + br * Kp + k0 + 16 * g4_swz(row, lch);
+            g4_glds(src, sB(st) + r16 * G4K);
+        }
+    };
+
+    v16i acc[3][2];
+#pragma unroll
+    for (int a = 0; a < 3; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++) acc[a][b] = v16i{0};
+
+    const int r = lane & 31, h = lane >> 5;
+    const int nk = Kp / G4K;
+    // prologue: steps 0, 1, 2 in flight
+    for (int ks = 0; ks < G4S - 1 && ks < nk; ks++) stage(ks, ks);
+    for (int ks = 0; ks < nk; ks++) {
+        // retire step ks (this wave's loads), keeping the loads of up to 2 later steps in flight;
+        // the barrier then publishes every wave's pieces and frees the stage read in step ks - 1
+        const int ahead = min(G4S - 2, nk - 1 - ks);
+        if (wave < 6) {
+            if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            if (ahead >= 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else if (ahead == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (ks + G4S - 1 < nk) stage((ks + G4S - 1) % G4S, ks + G4S - 1);
+        const int st = ks % G4S;
+        const int8_t *a_s = sA(st), *b_s = sB(st);
+        v4i fa[2][3], fb[2][2];  // both K halves of the step read up front
+#pragma unroll
+        for (int kk = 0; kk < G4K / 32; kk++) {
+#pragma unroll
+            for (int m = 0; m < 3; m++) {
+                const int row = wm * 96 + m * 32 + r;
+                fa[kk][m] = *reinterpret_cast<const v4i *>(a_s + row * G4K + 16 * g4_swz(row, 2 * kk + h));
+            }
+#pragma unroll
+            for (int tj = 0; tj < 2; tj++) {
+                const int row = wn * 64 + tj * 32 + r;
+                fb[kk][tj] = *reinterpret_cast<const v4i *>(b_s + row * G4K + 16 * g4_swz(row, 2 * kk + h));
+            }
+        }
+#pragma unroll
+        for (int kk = 0; kk < G4K / 32; kk++)
+#pragma unroll
+            for (int m = 0; m < 3; m++)
+#pragma unroll
+                for (int tj = 0; tj < 2; tj++)
+                    acc[m][tj] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[kk][m], fb[kk][tj], acc[m][tj], 0, 0, 0);
+    }
+
+    const int j = r & 7;
+    const long b0 = (mt * 2 + wm) * 32;
+#pragma unroll
+    for (int tj = 0; tj < 2; tj++) {
+        const long col = (col8_0 + wn * 64 + tj * 32 + r) >> 3;
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            uint64_t v = 0;
+#pragma unroll
+            for (int m = 0; m < 3; m++) {
+                const int sh = LB3 * m + 8 * j;
+                const uint64_t p = (uint64_t)(int64_t)acc[m][tj][q];
+                v += sh < 64 ? (p << sh) : 0;
+            }
+#pragma unroll
+            for (int x = 1; x < 8; x <<= 1) {
+                const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+                const uint32_t olo = __shfl_xor((int)lo, x, 64), ohi = __shfl_xor((int)hi, x, 64);
+                v += ((uint64_t)ohi << 32) | olo;
+            }
+            const long b = b0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+            if (j == 0 && col < ncols && b < B) out[b * out_stride + col] = 0 - v;
+        }
+    }
+}
+
+inline size_t gemm_g4_lds() { return (size_t)G4S * (G4A + G4B); }
+
 }  // namespace ksgemm
 }  // namespace tae
