@@ -518,7 +518,11 @@ inline size_t gemm_big3_lds() { return (size_t)2 * (B3M + BTN) * LROW; }
 // bank-conflict swizzle (16-byte chunk c of row r stored at c ^ ((r >> 2) & 3)) goes on the
 // per-lane global source address and on the fragment reads.  Same tiles, limbs and epilogue as
 // gemm_big3: bit-identical results. ----
+#ifndef TAE_G4S
 constexpr int G4K = 64, G4S = 4;                      // K bytes per step, ring stages
+#else
+constexpr int G4K = 64, G4S = TAE_G4S;
+#endif
 constexpr int G4A = B3M * G4K, G4B = BTN * G4K;       // bytes per stage
 __device__ __forceinline__ int g4_swz(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
 
@@ -584,20 +588,20 @@ __global__ void __launch_bounds__(512, 1)
 
     const int r = lane & 31, h = lane >> 5;
     const int nk = Kp / G4K;
-    // prologue: steps 0, 1, 2 in flight
+    // prologue: steps 0 .. G4S - 2 in flight
     for (int ks = 0; ks < G4S - 1 && ks < nk; ks++) stage(ks, ks);
     for (int ks = 0; ks < nk; ks++) {
         // retire step ks (this wave's loads), keeping the loads of up to 2 later steps in flight;
         // the barrier then publishes every wave's pieces and frees the stage read in step ks - 1
         const int ahead = min(G4S - 2, nk - 1 - ks);
-        if (wave < 6) {
-            if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-            else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        } else {
-            if (ahead >= 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            else if (ahead == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int nvm = (wave < 6 ? 4 : 2) * ahead;  // this wave's loads of the later steps
+        switch (nvm) {
+        case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
@@ -619,6 +623,9 @@ __global__ void __launch_bounds__(512, 1)
                 fb[kk][tj] = *reinterpret_cast<const v4i *>(b_s + row * G4K + 16 * g4_swz(row, 2 * kk + h));
             }
         }
+#ifdef TAE_G4_PRIO
+        __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
         for (int kk = 0; kk < G4K / 32; kk++)
 #pragma unroll
@@ -626,6 +633,9 @@ __global__ void __launch_bounds__(512, 1)
 #pragma unroll
                 for (int tj = 0; tj < 2; tj++)
                     acc[m][tj] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[kk][m], fb[kk][tj], acc[m][tj], 0, 0, 0);
+#ifdef TAE_G4_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
     }
 
     const int j = r & 7;
