@@ -27,6 +27,23 @@ __device__ __forceinline__ void s_setprio_c() {
 
 constexpr int N = 1024, M = 512, K1 = 3, C = 2, JOBS = C * K1, THREADS = 512;
 
+// TAE_B1K_PROF (debug builds only): per-phase cycle sums of every wave of workgroup 0
+#ifdef TAE_B1K_PROF
+#define BPROF_DECL uint64_t bprof_[6] = {0}, bprof_t_ = clock64();
+#define BPROF(i)                           \
+    do {                                   \
+        asm volatile("" ::: "memory");     \
+        const uint64_t now_ = clock64();   \
+        bprof_[i] += now_ - bprof_t_;      \
+        bprof_t_ = now_;                   \
+    } while (0)
+#else
+#define BPROF_DECL
+#define BPROF(i) \
+    do {         \
+    } while (0)
+#endif
+
 // a job's lanes are one wave and a wave's LDS operations execute in order: hand-offs inside a job
 // only need the compiler not to reorder
 __device__ __forceinline__ void wave_sync() { asm volatile("" ::: "memory"); }
@@ -129,6 +146,7 @@ __global__ void __launch_bounds__(THREADS, 1)
     uint64_t a_next = (PBS && jvalid) ? lwe_in[(size_t)(ct0 + jct) * (n + 1)] : 0;
     cplx accr[K1 * C];
     cplx gv[K1 * K1];
+    BPROF_DECL
     for (int step = 0; step < steps; step++) {
         s_setprio_c<2>();
         int e, gstep;
@@ -183,6 +201,7 @@ __global__ void __launch_bounds__(THREADS, 1)
         for (int a = 0; a < K1 * C; a++) accr[a] = cplx{0.0, 0.0};
 
 #pragma unroll(LEV <= 2 ? LEV : 1)
+        BPROF(0);
         for (int lev = LEV; lev >= 1; lev--) {
 #pragma unroll
             for (int p = 0; p < K1; p++)
@@ -248,7 +267,9 @@ __global__ void __launch_bounds__(THREADS, 1)
 #pragma unroll
                 for (int kk = 0; kk < 8; kk++) X[pidx(8 * tt + kk)] = v[kk];
             }
+            BPROF(1);
             br512::lds_sync();
+            BPROF(2);
             s_setprio_c<3>();
             // MAC at Fourier position pos: accumulator (q, c) = accr[q * C + c], p ascending
 #pragma unroll
@@ -271,7 +292,9 @@ __global__ void __launch_bounds__(THREADS, 1)
                         accr[q * C + c] = {re, im};
                     }
             }
+            BPROF(3);
             br512::lds_sync();
+            BPROF(2);
             s_setprio_c<3>();
         }
         // ---- inverse FFT of the MAC results, accumulated into ACC ----
@@ -324,7 +347,14 @@ __global__ void __launch_bounds__(THREADS, 1)
             }
         }
         wave_sync();
+        BPROF(4);
     }
+#ifdef TAE_B1K_PROF
+    if (blockIdx.x == 0 && (tid & 63) == 0)
+        printf("b1kprof wave %d: dec %llu fft %llu bar %llu mac %llu inv %llu\n", jb, (unsigned long long)bprof_[0],
+               (unsigned long long)bprof_[1], (unsigned long long)bprof_[2], (unsigned long long)bprof_[3],
+               (unsigned long long)bprof_[4]);
+#endif
     br512::lds_sync();
     for (int ct = 0; ct < nct; ct++) {
         const uint64_t *a = acc + ct * K1 * ACC_STRIDE;
