@@ -161,10 +161,12 @@ def test_aes8_full_fips197_with_fhe_key_schedule(gpu_context8, client8, golden):
     assert got == aes_128.expand_key_and_encrypt_blocks(key, blocks, 10)
 
 
-@pytest.mark.parametrize("pid", [tfhe_aes.PARAMS_SQRD_LVL_1, tfhe_aes.PARAMS_SQRD_LVL_256])
+@pytest.mark.parametrize("pid", [tfhe_aes.PARAMS_SQRD_LVL_1, tfhe_aes.PARAMS_SQRD_LVL_4,
+                                 tfhe_aes.PARAMS_SQRD_LVL_256])
 def test_other_n1024_sets_bit_exact(pid, oracle_mod):
-    """The batched N=1024 blind rotation (br1024.hpp) under params_sqrd_lvl_1 (pbs 2 x 2^15) and _256
-    (pbs 4 x 2^9): homomorphic_shift_boolean and a 4 -> 4 circuit bootstrap, equal to the oracle."""
+    """The batched N=1024 blind rotation (br1024.hpp) under params_sqrd_lvl_1 (pbs 2 x 2^15, pfks
+    1 x 2^24: scalar PFKS), _4 (pbs 2 x 2^15, pfks 2 x 2^16: int8 MFMA PFKS) and _256 (pbs 4 x 2^9):
+    homomorphic_shift_boolean and a 4 -> 4 circuit bootstrap, equal to the oracle."""
     ck, keys = tfhe_aes.generate_keys_raw(pid, SEED, threads=THREADS)
     ctx = tfhe_aes.context_from_raw(pid, keys, device=0)
     ok = oracle_mod.Keys(pid, None, raw=keys)
