@@ -150,7 +150,8 @@ class Engine {
     void collect_times();
     // int8 MFMA keyswitches (ksgemm.hpp): key limb matrices + digit scratch
     bool mfma_ks_ = false;
-    bool glds_gemm_ = true;   // PFKS on the LDS-DMA GEMM (ksgemm.hpp gemm_g4; TAE_GEMM_GLDS=0: gemm_big3)
+    bool pf_il_ = false;      // PFKS operands row-pair interleaved (ksgemm::op_off), for gemm_g6
+    int glds_gemm_ = 8;       // PFKS GEMM: 8 / 6 / 2 gemm_g6 (LDS-DMA; 4 / 3 / 2 M waves), 0 gemm_big3
     bool gemm3_ = true;     // PFKS digits as 3 x 6-bit limbs (TAE_GEMM_MA4=1: 4 x 5 bits)
     bool big_gemm_ = true;  // PFKS on the 256 x 256-tile GEMM (TAE_GEMM_SMALL=1: 128 x 128)
     int8_t *d_pf_bt_ = nullptr, *d_ks_bt_ = nullptr, *d_digits_ = nullptr;

@@ -729,10 +729,15 @@ void Engine::prepare_mfma_keys() {
                              (int)ksgemm::gemm_big_lds()));
     HIPC(hipFuncSetAttribute((const void *)ksgemm::gemm_big3<6>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)ksgemm::gemm_big3_lds()));
-    HIPC(hipFuncSetAttribute((const void *)ksgemm::gemm_g4<6>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)ksgemm::gemm_g4_lds()));
+    HIPC(hipFuncSetAttribute((const void *)ksgemm::gemm_g6<6, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)ksgemm::gemm_g6_lds<2>()));
+    HIPC(hipFuncSetAttribute((const void *)ksgemm::gemm_g6<6, 3>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)ksgemm::gemm_g6_lds<3>()));
+    HIPC(hipFuncSetAttribute((const void *)ksgemm::gemm_g6<6, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)ksgemm::gemm_g6_lds<4>()));
+    // TAE_GEMM_GLDS=0: register-staged gemm_big3; 2 / 6 / 8 (default): gemm_g6 with 2 / 3 / 4 M waves
     const char *gl = getenv("TAE_GEMM_GLDS");
-    glds_gemm_ = !(gl && gl[0] == '0');  // TAE_GEMM_GLDS=0: register-staged gemm_big3
+    glds_gemm_ = !gl ? 8 : gl[0] == '0' ? 0 : gl[0] == '2' ? 2 : gl[0] == '6' ? 6 : 8;
     const char *v = getenv("TAE_KS_VALU");
     mfma_ks_ = !(v && v[0] == '1') && p_.pfks_b * 1 <= 16 && p_.ks_b <= 7;
     if (!mfma_ks_) return;
@@ -744,15 +749,17 @@ void Engine::prepare_mfma_keys() {
     d_pf_bt_ = static_cast<int8_t *>(alloc((size_t)nc_pf * 8 * kp_pf_));
     d_ks_bt_ = static_cast<int8_t *>(alloc((size_t)nc_ks * 8 * kp_ks_));
     dim3 gpf((kp_pf_ + 63) / 64, (nc_pf + 63) / 64), gks((kp_ks_ + 63) / 64, (nc_ks + 63) / 64);
+    // the LDS-DMA GEMMs read both operands row-pair interleaved (ksgemm::op_off)
+    pf_il_ = big_gemm_ && gemm3_ && glds_gemm_ != 0 && kp_pf_ % ksgemm::G4K == 0;
     ksgemm::prep_key<<<gpf, kThreads, 0, stream_>>>(d_pfpksk_, d_pf_bt_, kd_pf, kp_pf_, nc_pf, glwe, glwe,
-                                                    (long)(p_.K() + 1) * p_.pfks_l * glwe);
+                                                    (long)(p_.K() + 1) * p_.pfks_l * glwe, pf_il_);
     ksgemm::prep_key<<<gks, kThreads, 0, stream_>>>(d_ksk_, d_ks_bt_, kd_ks, kp_ks_, nc_ks, nc_ks, nc_ks, 0);
     HIPC(hipGetLastError());
     HIPC(hipStreamSynchronize(stream_));
 }
 
 // digit scratch for B ciphertexts x rows_per_ct rows of Kp bytes (padding columns zeroed)
-static void ensure_digits(int8_t *&buf, size_t &cap, size_t rows, int Kd, int Kp, hipStream_t s) {
+static void ensure_digits(int8_t *&buf, size_t &cap, size_t rows, int Kd, int Kp, hipStream_t s, bool il = false) {
     const size_t need = rows * (size_t)Kp;
     if (need > cap) {
         if (buf) hip_check(hipFree(buf), "hipFree");
@@ -761,7 +768,7 @@ static void ensure_digits(int8_t *&buf, size_t &cap, size_t rows, int Kd, int Kp
     }
     if (Kp > Kd) {
         const size_t total = rows * (size_t)(Kp - Kd);
-        ksgemm::zero_pad<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(buf, (long)rows, Kd, Kp);
+        ksgemm::zero_pad<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(buf, (long)rows, Kd, Kp, il);
         hip_check(hipGetLastError(), "zero_pad");
     }
 }
@@ -904,20 +911,30 @@ void Engine::pfks_into_ggsw(const uint64_t *d_big, uint64_t *d_ggsw, size_t B, i
     if (mfma_ks_ && big_gemm_ && gemm3_) {
         // digits as 3 balanced 6-bit limbs, limb index in the MFMA row tile (ksgemm.hpp gemm_big3)
         const int K = p_.K(), kd = (K + 1) * p_.pfks_l;
-        const long mtiles = (long)((B + 63) / 64);
-        ensure_digits(d_digits_, cap_digits_, (size_t)mtiles * ksgemm::B3M, kd, kp_pf_, stream_);
+        // 192-, 288- and 384-row tiles (64, 96, 128 ciphertexts)
+        const long mtiles = (long)((B + 63) / 64), mt3 = (long)((B + 95) / 96), mt4 = (long)((B + 127) / 128);
+        const size_t rows = std::max({(size_t)mtiles * ksgemm::B3M, (size_t)mt3 * 288, (size_t)mt4 * 384});
+        ensure_digits(d_digits_, cap_digits_, rows, kd, kp_pf_, stream_, pf_il_);
         const size_t thr = B * (size_t)(K + 1);
         ksgemm::prep_digits3<6><<<(unsigned)((thr + 255) / 256), 256, 0, stream_>>>(
-            d_big, K + 1, d_digits_, (long)B, K + 1, kp_pf_, p_.pfks_b, p_.pfks_l);
+            d_big, K + 1, d_digits_, (long)B, K + 1, kp_pf_, p_.pfks_b, p_.pfks_l, pf_il_);
         const int ncols = (p_.k + 1) * glwe;
         const long out_stride = (long)p_.cbs_l * ncols;
         const long ntiles = ((long)ncols * 8 + ksgemm::BTN - 1) / ksgemm::BTN;
-        if (glds_gemm_ && kp_pf_ % ksgemm::G4K == 0)
-            ksgemm::gemm_g4<6><<<(unsigned)(mtiles * ntiles), 512, ksgemm::gemm_g4_lds(), stream_>>>(
-                d_digits_, d_pf_bt_, kp_pf_, mtiles, ncols, d_ggsw + (size_t)(level - 1) * ncols, out_stride, (long)B);
-        else
+        uint64_t *dst = d_ggsw + (size_t)(level - 1) * ncols;
+        if (pf_il_ && glds_gemm_ == 8) {
+            ksgemm::gemm_g6<6, 4><<<(unsigned)(mt4 * ntiles), 1024, ksgemm::gemm_g6_lds<4>(), stream_>>>(
+                d_digits_, d_pf_bt_, kp_pf_, mt4, ncols, dst, out_stride, (long)B);
+        } else if (pf_il_ && glds_gemm_ == 6) {
+            ksgemm::gemm_g6<6, 3><<<(unsigned)(mt3 * ntiles), 768, ksgemm::gemm_g6_lds<3>(), stream_>>>(
+                d_digits_, d_pf_bt_, kp_pf_, mt3, ncols, dst, out_stride, (long)B);
+        } else if (pf_il_) {
+            ksgemm::gemm_g6<6, 2><<<(unsigned)(mtiles * ntiles), 512, ksgemm::gemm_g6_lds<2>(), stream_>>>(
+                d_digits_, d_pf_bt_, kp_pf_, mtiles, ncols, dst, out_stride, (long)B);
+        } else {
             ksgemm::gemm_big3<6><<<(unsigned)(mtiles * ntiles), 512, ksgemm::gemm_big3_lds(), stream_>>>(
-                d_digits_, d_pf_bt_, kp_pf_, mtiles, ncols, d_ggsw + (size_t)(level - 1) * ncols, out_stride, (long)B);
+                d_digits_, d_pf_bt_, kp_pf_, mtiles, ncols, dst, out_stride, (long)B);
+        }
         HIPC(hipGetLastError());
         return;
     }

@@ -41,12 +41,20 @@ __device__ __forceinline__ void key_limbs(uint64_t k, int8_t *lb) {
     }
 }
 
+// Operand layouts in HBM.  Row-major: element (row, k) at row * Kp + k.  Row-pair interleaved
+// (the LDS-DMA GEMMs gemm_g4 / gemm_g5): rows 2i and 2i + 1 share each 128-byte line, 64 K bytes of
+// each, so one 64-byte K step of a row pair is one whole cache line (one L2 request instead of two
+// half-line requests issued a K step apart).  Needs Kp % 64 == 0 and an even row count.
+__host__ __device__ __forceinline__ long op_off(long row, long k, int Kp, bool il) {
+    return il ? (row >> 1) * 2 * Kp + (k >> 6) * 128 + (row & 1) * 64 + (k & 63) : row * Kp + k;
+}
+
 // ---- key preparation: u64 key rows -> Bt[(col * 8 + j) * Kp + kd] (int8) ----
 // key element for (kd, col) at key[kd * key_kd_stride + (col / cols_per_block) * key_blk_stride +
 // col % cols_per_block]; used for both PFPKSK ([q][i][l][glwe]) and KSK ([i][l][n+1]).
 __global__ void __launch_bounds__(256) prep_key(const uint64_t *__restrict__ key, int8_t *__restrict__ Bt, int Kd, int Kp,
                                                 int ncols, int cols_per_block, long key_kd_stride,
-                                                long key_blk_stride) {
+                                                long key_blk_stride, bool il = false) {
     __shared__ int8_t tile[64][8][65];
     const int kd0 = blockIdx.x * 64, col0 = blockIdx.y * 64;
     // load 64 kd x 64 cols (col fastest, coalesced), split into limbs
@@ -68,7 +76,7 @@ __global__ void __launch_bounds__(256) prep_key(const uint64_t *__restrict__ key
         const int kk = t & 63, row = t >> 6;  // row = cc * 8 + j
         const int cc = row >> 3, j = row & 7;
         const int col = col0 + cc, kd = kd0 + kk;
-        if (col < ncols && kd < Kp) Bt[((long)col * 8 + j) * Kp + kd] = tile[cc][j][kk];
+        if (col < ncols && kd < Kp) Bt[op_off((long)col * 8 + j, kd, Kp, il)] = tile[cc][j][kk];
     }
 }
 
@@ -110,11 +118,11 @@ __global__ void __launch_bounds__(256) prep_digits(const uint64_t *__restrict__ 
 }
 
 // zero the padding columns kd in [Kd, Kp) of every row (done once per buffer size change)
-__global__ void zero_pad(int8_t *A, long rows, int Kd, int Kp) {
+__global__ void zero_pad(int8_t *A, long rows, int Kd, int Kp, bool il = false) {
     const long t = (long)blockIdx.x * 256 + threadIdx.x;
     const int w = Kp - Kd;
     const long r = t / w;
-    if (r < rows) A[r * Kp + Kd + (int)(t - r * w)] = 0;
+    if (r < rows) A[op_off(r, Kd + (t - r * w), Kp, il)] = 0;
 }
 
 // ---- the GEMM ----
@@ -359,7 +367,7 @@ inline size_t gemm_big_lds() { return (size_t)2 * (BTM + BTN) * LROW; }
 template <int LB3>
 __global__ void __launch_bounds__(256) prep_digits3(const uint64_t *__restrict__ in, long in_stride,
                                                     int8_t *__restrict__ A, long B, int n_in, int Kp, int base_log,
-                                                    int levels) {
+                                                    int levels, bool il = false) {
     const long t = (long)blockIdx.x * 256 + threadIdx.x;
     const long b = t / n_in;
     const int i = (int)(t - b * n_in);
@@ -388,7 +396,7 @@ __global__ void __launch_bounds__(256) prep_digits3(const uint64_t *__restrict__
                 limb = ((d + (1 << (LB3 - 1))) & ((1 << LB3) - 1)) - (1 << (LB3 - 1));
                 d = (d - limb) >> LB3;
             }
-            A[(rbase + 32 * m) * Kp + kd] = (int8_t)limb;
+            A[op_off(rbase + 32 * m, kd, Kp, il)] = (int8_t)limb;
         }
     }
 }
@@ -511,19 +519,25 @@ __global__ void __launch_bounds__(512, 1)
 
 inline size_t gemm_big3_lds() { return (size_t)2 * (B3M + BTN) * LROW; }
 
-// ---- gemm_big3 with LDS-DMA staging: global_load_lds (16 B per lane, no VGPR staging, no
-// ds_write) into a 4-stage ring of 64-byte K steps, two steps kept in flight across the per-step
-// barrier by a counted vmcnt (cdna_hip_programming.md section 5: "Async global->LDS copy",
-// "Pipelining across barriers").  The LDS image is lane-linear (rows of 64 B, no padding), so the
-// bank-conflict swizzle (16-byte chunk c of row r stored at c ^ ((r >> 2) & 3)) goes on the
-// per-lane global source address and on the fragment reads.  Same tiles, limbs and epilogue as
-// gemm_big3: bit-identical results. ----
+// ---- gemm_g6: the gemm_big3 product with LDS-DMA staging (default PFKS GEMM) ----
+// - Staging: global_load_lds (16 B per lane, no VGPR staging, no ds_write) into a ring of G4S stages
+//   of 64-byte K steps; two steps stay in flight across the per-step barrier by a counted vmcnt
+//   (cdna_hip_programming.md section 5: "Async global->LDS copy", "Pipelining across barriers").
+// - The LDS image is lane-linear (rows of 64 B, no padding), so the bank-conflict swizzle (16-byte
+//   chunk c of row r stored at c ^ ((r >> 2) & 3)) goes on the per-lane global source address and
+//   on the fragment reads.
+// - Operands row-pair interleaved in HBM (op_off): one K step of two rows is one 128-byte line.
+// - WM x 4 waves of 96 x 64 (3 limbs x 32 ciphertexts by 64 key columns), workgroup tile
+//   96 WM x 256.  WM = 4 (default, 1024 threads, 384 x 256, 160 KiB ring) moves 30% fewer operand
+//   bytes per MFMA than WM = 2 (192 x 256) and runs four MFMA streams per SIMD: 22.5 -> 20.1 ms per
+//   16384-ciphertext launch (WM = 3: 21.0).  The 6 WM + 16 pieces of 16 rows per stage are dealt
+//   round-robin over the waves.
+// - Same limbs and epilogue as gemm_big3: bit-identical results.
 #ifndef TAE_G4S
 constexpr int G4K = 64, G4S = 4;                      // K bytes per step, ring stages
 #else
 constexpr int G4K = 64, G4S = TAE_G4S;
 #endif
-constexpr int G4A = B3M * G4K, G4B = BTN * G4K;       // bytes per stage
 __device__ __forceinline__ int g4_swz(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
 
 // global_load_lds_dwordx4: 16 bytes per lane from src to lds_base + 16 * lane (lds_base wave-uniform).
@@ -537,10 +551,16 @@ __device__ __forceinline__ void g4_glds(const int8_t *src, int8_t *lds_base) {
 #endif
 }
 
-template <int LB3>
-__global__ void __launch_bounds__(512, 1)
-    gemm_g4(const int8_t *__restrict__ A, const int8_t *__restrict__ Bt, int Kp, long mtiles, int ncols,
+template <int WM>
+inline size_t gemm_g6_lds() { return (size_t)G4S * (96 * WM + BTN) * G4K; }
+
+template <int LB3, int WM>
+__global__ void __launch_bounds__(256 * WM, 1)
+    gemm_g6(const int8_t *__restrict__ A, const int8_t *__restrict__ Bt, int Kp, long mtiles, int ncols,
             uint64_t *__restrict__ out, long out_stride, long B) {
+    constexpr int TMR = 96 * WM, NW = 4 * WM;              // tile rows, waves
+    constexpr int SA = TMR * G4K, SAB = (TMR + BTN) * G4K;  // stage bytes
+    constexpr int NPA = TMR / 16, NP = NPA + BTN / 16;      // 16-row pieces per stage
     extern __shared__ __align__(16) int8_t smem_g[];
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int wm = wave >> 2, wn = wave & 3;
@@ -550,33 +570,39 @@ __global__ void __launch_bounds__(512, 1)
     const long ng = blockIdx.x / gsz, rr = blockIdx.x - ng * gsz;
     const long gw = min(GN, ntiles - ng * GN);
     const long mt = rr / gw, nt = ng * GN + (rr - (rr / gw) * gw);
-    const long row0 = mt * B3M;
+    const long row0 = mt * TMR;
     const long col8_0 = nt * BTN;
     const long N8 = (long)ncols * 8;
-    auto sA = [&](int st) { return smem_g + st * (G4A + G4B); };
-    auto sB = [&](int st) { return smem_g + st * (G4A + G4B) + G4A; };
 
-    // one glds wave-instruction = 16 rows x 4 chunks (1 KiB).  Per stage: A 12 of them (waves 0-5
-    // issue 2), B 16 (every wave 2) -> 4 or 2 per wave
     const int lrow = lane >> 2, lch = lane & 3;
     auto stage = [&](int st, int ks) {
         const int k0 = ks * G4K;
-        if (wave < 6) {
+        int8_t *base = smem_g + st * SAB;
 #pragma unroll
-            for (int t = 0; t < 2; t++) {
-                const int r16 = (wave * 2 + t) * 16;  // first row of this piece
-                const int row = r16 + lrow;
-                const int8_t *src = A + (row0 + row) * Kp + k0 + 16 * g4_swz(row, lch);
-                g4_glds(src, sA(st) + r16 * G4K);
+        for (int p = wave; p < NP; p += NW) {  // piece p: rows 16 p .. 16 p + 15 of the stage image
+            const int row = 16 * p + lrow;
+            const int8_t *src;
+            if (p < NPA) {
+                src = A + op_off(row0 + row, k0, Kp, true) + 16 * g4_swz(row, lch);
+            } else {
+                const int rb = row - TMR;
+                const long br = min(col8_0 + rb, N8 - 1);  // rows past the last column feed unstored outputs
+                src = Bt + op_off(br, k0, Kp, true) + 16 * g4_swz(rb, lch);
             }
+            g4_glds(src, base + 16 * p * G4K);
         }
-#pragma unroll
-        for (int t = 0; t < 2; t++) {
-            const int r16 = (wave * 2 + t) * 16;
-            const int row = r16 + lrow;
-            const long br = min(col8_0 + row, N8 - 1);  // rows past the last column feed unstored outputs
-            const int8_t *src = Bt + br * Kp + k0 + 16 * g4_swz(row, lch);
-            g4_glds(src, sB(st) + r16 * G4K);
+    };
+    const int per_wave = (NP / NW) + (wave < NP % NW ? 1 : 0);
+    auto wait_steps = [&](int keep) {  // retire all but this wave's loads of `keep` later steps
+        switch (per_wave * keep) {
+        case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+        case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
         }
     };
 
@@ -588,28 +614,15 @@ __global__ void __launch_bounds__(512, 1)
 
     const int r = lane & 31, h = lane >> 5;
     const int nk = Kp / G4K;
-    // prologue: steps 0 .. G4S - 2 in flight
     for (int ks = 0; ks < G4S - 1 && ks < nk; ks++) stage(ks, ks);
     for (int ks = 0; ks < nk; ks++) {
-        // retire step ks (this wave's loads), keeping the loads of up to 2 later steps in flight;
-        // the barrier then publishes every wave's pieces and frees the stage read in step ks - 1
-        const int ahead = min(G4S - 2, nk - 1 - ks);
-        const int nvm = (wave < 6 ? 4 : 2) * ahead;  // this wave's loads of the later steps
-        switch (nvm) {
-        case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-        }
+        wait_steps(min(G4S - 2, nk - 1 - ks));
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
         if (ks + G4S - 1 < nk) stage((ks + G4S - 1) % G4S, ks + G4S - 1);
-        const int st = ks % G4S;
-        const int8_t *a_s = sA(st), *b_s = sB(st);
-        v4i fa[2][3], fb[2][2];  // both K halves of the step read up front
+        const int8_t *a_s = smem_g + (ks % G4S) * SAB, *b_s = a_s + SA;
+        v4i fa[2][3], fb[2][2];
 #pragma unroll
         for (int kk = 0; kk < G4K / 32; kk++) {
 #pragma unroll
@@ -623,9 +636,6 @@ __global__ void __launch_bounds__(512, 1)
                 fb[kk][tj] = *reinterpret_cast<const v4i *>(b_s + row * G4K + 16 * g4_swz(row, 2 * kk + h));
             }
         }
-#ifdef TAE_G4_PRIO
-        __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
         for (int kk = 0; kk < G4K / 32; kk++)
 #pragma unroll
@@ -633,13 +643,10 @@ __global__ void __launch_bounds__(512, 1)
 #pragma unroll
                 for (int tj = 0; tj < 2; tj++)
                     acc[m][tj] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[kk][m], fb[kk][tj], acc[m][tj], 0, 0, 0);
-#ifdef TAE_G4_PRIO
-        __builtin_amdgcn_s_setprio(0);
-#endif
     }
 
     const int j = r & 7;
-    const long b0 = (mt * 2 + wm) * 32;
+    const long b0 = (mt * WM + wm) * 32;
 #pragma unroll
     for (int tj = 0; tj < 2; tj++) {
         const long col = (col8_0 + wn * 64 + tj * 32 + r) >> 3;
@@ -663,8 +670,6 @@ __global__ void __launch_bounds__(512, 1)
         }
     }
 }
-
-inline size_t gemm_g4_lds() { return (size_t)G4S * (G4A + G4B); }
 
 }  // namespace ksgemm
 }  // namespace tae
