@@ -564,10 +564,23 @@ __global__ void __launch_bounds__(256 * WM, 1)
     extern __shared__ __align__(16) int8_t smem_g[];
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int wm = wave >> 2, wn = wave & 3;
-    constexpr long GN = 16;
     const long ntiles = (((long)ncols * 8) + BTN - 1) / BTN;
+#ifndef TAE_G6_GN
+    constexpr long GN = 8;
+#else
+    constexpr long GN = TAE_G6_GN;
+#endif
+#ifndef TAE_G6_NOXCD
+    // XCD-aware order (cdna_hip_programming.md T1, bijective form): blocks b, b + 8, b + 16, ... run
+    // on one XCD, so give them a contiguous range of the grouped tile order; its ~32 co-resident
+    // tiles are then 4 M tiles x GN (= 8) N tiles sharing their operand K slices in that XCD's L2
+    const long nwg = (long)gridDim.x, q8 = nwg >> 3, r8 = nwg & 7, x8 = blockIdx.x & 7;
+    const long bid = x8 * q8 + min(x8, r8) + (blockIdx.x >> 3);
+#else
+    const long bid = blockIdx.x;
+#endif
     const long gsz = GN * mtiles;
-    const long ng = blockIdx.x / gsz, rr = blockIdx.x - ng * gsz;
+    const long ng = bid / gsz, rr = bid - ng * gsz;
     const long gw = min(GN, ntiles - ng * GN);
     const long mt = rr / gw, nt = ng * GN + (rr - (rr / gw) * gw);
     const long row0 = mt * TMR;
