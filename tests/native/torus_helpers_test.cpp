@@ -50,6 +50,19 @@ static void check_dec(uint64_t x, int B) {
     }
 }
 
+// packed two-coefficient decomposition == decompose16 on each half
+template <int LEV, int B>
+static void check_decp(uint64_t x0, uint64_t x1) {
+    uint32_t d[LEV], a[LEV], b[LEV];
+    tae::decompose16p<LEV, B>(x0, x1, d);
+    tae::decompose16t<LEV, B>(x0, a);
+    tae::decompose16t<LEV, B>(x1, b);
+    for (int l = 0; l < LEV; l++)
+        if (d[l] != (a[l] | (b[l] << 16)) && fails++ < 10)
+            printf("decompose16p(%016llx, %016llx, B=%d, L=%d) level %d: got %08x want %08x\n", (unsigned long long)x0,
+                   (unsigned long long)x1, B, LEV, l + 1, d[l], a[l] | (b[l] << 16));
+}
+
 int main(int argc, char **argv) {
     const long n = argc > 1 ? atol(argv[1]) : 2000000;
     std::mt19937_64 rng(12345);
@@ -102,7 +115,20 @@ int main(int argc, char **argv) {
         check_dect<4, 6>(x);
         check_dect<3, 12>(x);
         check_dect<4, 9>(x);
+        const uint64_t y = (i & 2) ? rng() : (x ^ (rng() & 0xFFFFFFFull));
+        check_decp<3, 12>(x, y);
+        check_decp<1, 13>(x, y);
+        check_decp<6, 7>(x, y);
+        check_decp<4, 6>(x, y);
+        check_decp<4, 9>(x, y);
+        check_decp<2, 15>(x, y);
     }
+    for (uint64_t x : edges)
+        for (uint64_t y : edges) {
+            check_decp<3, 12>(x, y);
+            check_decp<1, 13>(x, y);
+            check_decp<6, 7>(x, y);
+        }
     printf("%s (%d mismatches)\n", fails ? "FAIL" : "OK", fails);
     return fails ? 1 : 0;
 }

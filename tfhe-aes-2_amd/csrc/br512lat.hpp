@@ -157,12 +157,11 @@ __global__ void __launch_bounds__(THREADS, 1)
             const uint64_t v0 = poly[ph], v1 = poly[ph ^ M];
             const uint64_t p0 = poly[j], p1 = poly[j + M];
             const uint64_t x0 = (v0 ^ m0) - (p0 + m0), x1 = (v1 ^ m1) - (p1 + m1);
-            uint32_t d0[LEV], d1[LEV];
-            decompose16<LEV>(x0, BLOG, d0);
-            decompose16<LEV>(x1, BLOG, d1);
-            mydig[i] = d0[0] | (d1[0] << 16);
+            uint32_t dp[LEV];
+            decompose16p<LEV, BLOG>(x0, x1, dp);
+            mydig[i] = dp[0];
 #pragma unroll
-            for (int l = 1; l < LEV; l++) s_dig[(((l - 1) * K1 + jb) * 4 + i) * 64 + ll] = d0[l] | (d1[l] << 16);
+            for (int l = 1; l < LEV; l++) s_dig[(((l - 1) * K1 + jb) * 4 + i) * 64 + ll] = dp[l];
         }
     };
     if (jb < K1 && n > 0) decompose_poly(mod_switch(in[0], LOGN) % (2 * N));

@@ -268,18 +268,21 @@ __global__ void __launch_bounds__(THREADS, 1)
                 const uint64_t v0 = poly[ph], v1 = poly[ph ^ M];
                 const uint64_t p0 = poly[j], p1 = poly[j + M];
                 const uint64_t x0 = (v0 ^ m0) - (p0 + m0), x1 = (v1 ^ m1) - (p1 + m1);
-                uint32_t d0[LEV], d1[LEV];
 #ifdef TAE_DBG_NODEC
-                for (int l = 0; l < LEV; l++) {
-                    d0[l] = (uint32_t)x0 & 0x7ff;
-                    d1[l] = (uint32_t)x1 & 0x7ff;
-                }
-#else
+                for (int l = 0; l < LEV; l++) dig[l][i] = ((uint32_t)x0 & 0x7ff) | (((uint32_t)x1 & 0x7ff) << 16);
+#elif defined(TAE_DEC_SCALAR)
+                uint32_t d0[LEV], d1[LEV];
                 decompose16<LEV>(x0, BLOG, d0);
                 decompose16<LEV>(x1, BLOG, d1);
-#endif
 #pragma unroll
                 for (int l = 0; l < LEV; l++) dig[l][i] = d0[l] | (d1[l] << 16);
+#else
+                // both halves at once with 16-bit SIMD ops (fft_device.hpp decompose16p)
+                uint32_t dp[LEV];
+                decompose16p<LEV, BLOG>(x0, x1, dp);
+#pragma unroll
+                for (int l = 0; l < LEV; l++) dig[l][i] = dp[l];
+#endif
             }
         }
 #pragma unroll

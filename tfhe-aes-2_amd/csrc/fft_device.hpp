@@ -207,6 +207,77 @@ __host__ __device__ __forceinline__ void decompose16t(uint64_t x, uint32_t *d) {
     }
 }
 
+// ---- packed two-coefficient decomposition (v_pk_* 16-bit SIMD) ----
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__host__ __device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+__host__ __device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+// v_perm_b32 / v_alignbit_b32 (host emulation for the native tests); perm selectors < 8 only
+__host__ __device__ __forceinline__ uint32_t perm_b32(uint32_t s0, uint32_t s1, uint32_t sel) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __builtin_amdgcn_perm(s0, s1, sel);
+#else
+    const uint64_t v = ((uint64_t)s0 << 32) | s1;
+    uint32_t r = 0;
+    for (int k = 0; k < 4; k++) r |= (uint32_t)((v >> (8 * ((sel >> (8 * k)) & 7))) & 0xff) << (8 * k);
+    return r;
+#endif
+}
+__host__ __device__ __forceinline__ uint32_t alignbit_b32(uint32_t hi, uint32_t lo, int s) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __builtin_amdgcn_alignbit(hi, lo, s);
+#else
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> s);
+#endif
+}
+
+// decompose16 of two coefficients at once, d[l] = digit of x0 | digit of x1 << 16 (the packed
+// layout the FFT passes read), with 16-bit SIMD ops on both halves.  Same digits as decompose16:
+// with F_i the B-bit fields of X = x + 2^(nrb-1) above bit nrb (F_0 lowest), the state at field i
+// is G_i = F_i + k_i (k_0 = 0), res_i = G_i mod 2^B, ovf_i = G_i >> B, and the carry rule reads bit
+// B-1 of the state above, i.e. of F_{i+1} + ovf_i; then k_{i+1} = ovf_i + c_i <= 1 (ovf_i = 1
+// forces res_i = 0, so c_i = 0).  The top state above the last field is ovf <= 1: bit B-1 clear.
+template <int LEV, int B>
+__host__ __device__ __forceinline__ void decompose16p(uint64_t x0, uint64_t x1, uint32_t *d) {
+    static_assert(B <= 15 && B * LEV <= 64 && B >= 2, "decompose16p shape");
+    constexpr int nrb = 64 - B * LEV;
+    const uint64_t X0 = x0 + (1ull << (nrb - 1)), X1 = x1 + (1ull << (nrb - 1));
+    constexpr uint32_t MASK = ((1u << B) - 1) * 0x10001u;
+    uint32_t F[LEV];
+    if constexpr (LEV == 3 && B == 12) {
+        // fields at bits 28..39, 40..51, 52..63: F0 straddles the dwords, F1 / F2 are bytes 1-2 / 2-3
+        const uint32_t h0 = (uint32_t)(X0 >> 32), h1 = (uint32_t)(X1 >> 32);
+        const uint32_t a0 = alignbit_b32(h0, (uint32_t)X0, 28), a1 = alignbit_b32(h1, (uint32_t)X1, 28);
+        F[0] = perm_b32(a1, a0, 0x05040100u) & MASK;
+        F[1] = perm_b32(h1, h0, 0x06050201u) & MASK;
+        F[2] = as_u32(as_u16x2(perm_b32(h1, h0, 0x07060302u)) >> (unsigned short)4);
+    } else {
+#pragma unroll
+        for (int i = 0; i < LEV; i++)
+            F[i] = ((uint32_t)(X0 >> (nrb + B * i)) & ((1u << B) - 1)) |
+                   (((uint32_t)(X1 >> (nrb + B * i)) & ((1u << B) - 1)) << 16);
+    }
+    const u16x2 one = {1, 1}, sh = {B, B}, shm = {B - 1, B - 1};
+    const u16x2 neg = {(unsigned short)(0x10000u - (1u << B)), (unsigned short)(0x10000u - (1u << B))};
+    u16x2 k = {0, 0};
+#pragma unroll
+    for (int i = 0; i < LEV; i++) {
+        u16x2 res, nxt;
+        if (i == 0) {
+            res = as_u16x2(F[0]);
+            nxt = LEV > 1 ? as_u16x2(F[1]) : u16x2{0, 0};
+        } else {
+            const u16x2 g = as_u16x2(F[i]) + k;
+            res = as_u16x2(as_u32(g) & MASK);
+            const u16x2 ovf = g >> sh;
+            nxt = i + 1 < LEV ? as_u16x2(F[i + 1]) + ovf : u16x2{0, 0};
+            k = ovf;
+        }
+        const u16x2 c = as_u16x2(((as_u32(res - one) | as_u32(nxt)) & as_u32(res))) >> shm;
+        d[LEV - 1 - i] = as_u32(res + c * neg);
+        if (i == 0) k = c; else k = k + c;
+    }
+}
+
 // pbs_modulus_switch: round(x * 2N / 2^64) in [0, 2N]
 __device__ __forceinline__ int mod_switch(uint64_t x, int logN) {
     uint64_t o = x >> (64 - logN - 2);
