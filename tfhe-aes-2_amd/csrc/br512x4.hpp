@@ -349,7 +349,11 @@ __global__ void __launch_bounds__(THREADS, 1)
             default: mac_level<3>(buf, pidx(pos), accr, gv); break;
             }
 #endif
+#ifdef TAE_DBG_NOBAR3
+            wave_sync();
+#else
             PROF_SYNC(3);
+#endif
             PRIO(3);
         }
         // ---- inverse FFT of the MAC results, accumulated into ACC ----
