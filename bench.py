@@ -57,13 +57,19 @@ def main():
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--key-schedule", choices=["fhe", "plain"], default="fhe")
     ap.add_argument("--cpu-baseline", choices=["auto", "on", "off"], default="auto")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0: this process's CPU share, capped by OMP_NUM_THREADS)")
     ap.add_argument("--single-block", choices=["auto", "on", "off"], default="auto",
                     help="also time one block alone (BASELINE configs[1]: 16 SBOX x 10 rounds on 1 GPU); "
                          "auto = on at world size 1")
     ap.add_argument("--model", choices=["1bit", "8bit"], default="1bit",
                     help="1bit: ShortintWoppbs1BitSboxGalMulPbsAesEncrypt (params_sqrd_lvl_64, the metric); "
                          "8bit: ShortintWoppbs8BitSboxPbsAesEncrypt (BASELINE config #5)")
+    ap.add_argument("--model8-leg", choices=["auto", "on", "off"], default="auto",
+                    help="with --model 1bit: also time BASELINE config #5 (8-bit model) on a bounded batch "
+                         "(--model8-blocks blocks, one step) and report it beside the headline line; auto = on "
+                         "at world size 1")
+    ap.add_argument("--model8-blocks", type=int, default=16)
     args = ap.parse_args()
     PBS_KERNEL = PBS_KERNELS[args.model]
 
@@ -120,7 +126,7 @@ def main():
                 aes_128.key_schedule_plain(README_KEY)), "FHE key schedule mismatch"
         else:
             ek = b"".join(aes_128.key_schedule_plain(README_KEY))
-            rk_np = ck.encrypt_bits_raw([b for byte in ek for b in aes_128.u8_to_bits(byte)], start_index=1 << 40)
+            rk_np = ck.encrypt_bits_raw([b for byte in ek for b in aes_128.u8_to_bits(byte)])  # fresh indices
     key_expansion_s = time.time() - t
     if rank == 0:
         rk_dev = torch.from_numpy(rk_np.view(np.int64)).to(f"cuda:{dev}")
@@ -201,11 +207,22 @@ def main():
     ms_per_step = elapsed * 1000.0 / args.steps
 
     # ---- roofline of the dominant kernel (PBS = homomorphic_shift_boolean blind rotation) ----
+    # Its own launches (ctx timing "pbs_main": the throughput kernel alone, HIP events on the engine
+    # stream around each launch) give the roofline; the whole PBS stage (plus the small-batch
+    # remainder kernel) is reported beside it.
     launches = stage_ms.get("pbs_launches", 0)
     pbs_ms = stage_ms.get("pbs", 0.0) / max(launches, 1)
+    main_ms = stage_ms.get("pbs_main", 0.0) / max(launches, 1)
+    main_cts = stage_ms.get("pbs_main_cts", 0.0) / max(launches, 1)
     bytes_launch, flop_launch = pbs_algorithmic(p, nb * 16 * 8)
-    gbs = bytes_launch / (pbs_ms * 1e-3) / 1e9 if pbs_ms > 0 else None
-    tflops = flop_launch / (pbs_ms * 1e-3) / 1e12 if pbs_ms > 0 else None
+    if main_ms > 0 and main_cts > 0:  # 1-bit model: br512x4 launches
+        k_bytes, k_flop = pbs_algorithmic(p, int(main_cts))
+        k_ms = main_ms
+    else:  # one kernel covers the whole stage
+        k_bytes, k_flop, k_ms = bytes_launch, flop_launch, pbs_ms
+    gbs = k_bytes / (k_ms * 1e-3) / 1e9 if k_ms > 0 else None
+    tflops = k_flop / (k_ms * 1e-3) / 1e12 if k_ms > 0 else None
+    stage_tflops = flop_launch / (pbs_ms * 1e-3) / 1e12 if pbs_ms > 0 else None
     # HBM traffic per launch of the same kernel from the committed PMC pass (scripts/bench_profile.sh
     # -> scripts/prof_summary.py: 2 x FETCH_SIZE + WRITE_SIZE), valid only for the same batch shape.
     traffic, traffic_src, traffic_dram = None, None, None
@@ -217,22 +234,31 @@ def main():
         if pm.get("blocks_per_gpu") == nb and "hbm_bytes_per_launch" in ent:
             traffic, traffic_src = ent["hbm_bytes_per_launch"], pm.get("source")
             traffic_dram = ent.get("hbm_dram_bytes_per_launch")
-    # The batched blind rotation is FP64-bound (>= 10 flop/B at any batch); its roofline
-    # is the chip's dense f64 peak (MFMA and VALU alike on MI355X), HBM figures ride along.
-    roofline = {"bound": "mfma", "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+    # The batched blind rotation is bound by the FP64 vector ALU (>= 10 flop/B at any
+    # batch; no MFMA on this path): peak = the dense FP64 vector rate, HBM figures ride along.
+    roofline = {"bound": "fp64_valu", "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": (tflops / FP64_PEAK_TFLOPS) if tflops else None, "traffic": traffic,
                 "traffic_unit": "bytes/launch", "traffic_source": traffic_src, "traffic_dram": traffic_dram,
-                "kernel": PBS_KERNEL + " (homomorphic_shift_boolean blind rotation)", "avg_launch_ms": pbs_ms,
-                "algorithmic_flop_per_launch": flop_launch,
+                "kernel": PBS_KERNEL + " (homomorphic_shift_boolean blind rotation)", "avg_launch_ms": k_ms,
+                "ciphertexts_per_launch": main_cts if main_ms > 0 else nb * 16 * 8,
+                "algorithmic_flop_per_launch": k_flop,
+                "stage": {"avg_ms": pbs_ms, "ciphertexts": nb * 16 * 8, "achieved": stage_tflops,
+                          "frac": (stage_tflops / FP64_PEAK_TFLOPS) if stage_tflops else None,
+                          "note": "whole PBS stage per launch: the kernel above + the br512lat remainder"},
                 "hbm": {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": (gbs / HBM_PEAK_GBS) if gbs else None,
-                        "algorithmic_bytes_per_launch": bytes_launch}}
-    stage_share = {k: v / args.steps for k, v in stage_ms.items() if k != "pbs_launches"}
+                        "algorithmic_bytes_per_launch": k_bytes}}
+    stage_share = {k: v / args.steps for k, v in stage_ms.items() if k not in ("pbs_launches", "pbs_main_cts")}
 
     cpu = None
     want_cpu = args.cpu_baseline == "on" or (args.cpu_baseline == "auto" and world == 1)
     if want_cpu and rank == 0:
-        cpu = cpu_baseline(raw, ck, min(args.cpu_threads, os.cpu_count() or 1), args.model)
+        cpu = cpu_baseline(raw, ck, args.cpu_threads or cpu_share(), args.model, rk_np)
+
+    model8 = None
+    want8 = args.model == "1bit" and (args.model8_leg == "on" or (args.model8_leg == "auto" and world == 1))
+    if want8 and rank == 0:
+        model8 = model8_leg(torch, dev, args.model8_blocks, threads)
 
     if rank == 0:
         rec = {"metric": "FHE AES-128 blocks/sec", "value": value, "unit": "blocks/s", "n_gpus": world,
@@ -248,36 +274,92 @@ def main():
                "roofline": roofline, "cpu_baseline": cpu,
                "stage_ms_per_step": stage_share, "per_sbox_ms": ms_per_step / (nb * 16 * args.rounds),
                "keygen_s": keygen_s, "key_setup_s": key_setup_s, "key_expansion_s": key_expansion_s,
-               "encrypt_s": encrypt_s, "correct": bool(ok), "single_block": single}
+               "encrypt_s": encrypt_s, "correct": bool(ok), "single_block": single, "model8": model8}
         print(json.dumps(rec), flush=True)
     if dist:
         dist.destroy_process_group()
 
 
-def cpu_baseline(raw, ck, threads, model="1bit", min_s=10.0):
-    """CPU oracle (restatement, kind "port") on a bounded sample of the same workload: the 16 SBOX
-    circuit bootstraps of one AES round of one block, threads over bytes as the reference's rayon
-    (fhe_sbox_gal_mul_pbs.rs:33-41, fhe_sbox_pbs.rs:23-31); blocks/s = 1 / (10 x round time)."""
+def cpu_share():
+    """Threads for the CPU baseline: this process's CPU share (affinity mask), capped by
+    OMP_NUM_THREADS where the job scheduler sets it (the GPU box gives a 1-GPU job 16 host threads
+    while os.cpu_count() reports the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = os.environ.get("OMP_NUM_THREADS")
+    if cap and cap.isdigit() and int(cap) > 0:
+        n = min(n, int(cap))
+    return max(1, n)
+
+
+def cpu_baseline(raw, ck, threads, model="1bit", rk=None):
+    """CPU oracle (restatement, kind "port": tfhe-rs is absent here) timed on this process's host cores:
+    one full 10-round block (fhe_sbox_gal_mul_pbs::encrypt_block_for_rounds) measured directly, the 16
+    SBOX circuit bootstraps of each round run on `threads` threads as the reference's rayon splits a
+    block's bytes (fhe_sbox_gal_mul_pbs.rs:33-41; the 8 extract-bit keyswitches of each SBOX are a
+    negligible share).  At N = 128 the reference's rayon over blocks (main.rs:148-152) keeps the same
+    cores busy, so its throughput is extrapolated from the per-block time at the same core count."""
     from oracle import oracle
     from tfhe_aes import aes_128
     ok = oracle.Keys(oracle.PARAMS_SQRD_LVL_64 if model == "1bit" else oracle.PARAMS_WOPPBS_8BIT, None, raw=raw)
     blk = README_IV + (1).to_bytes(8, "big")
-    cts = ck.encrypt_bits_raw(aes_128.blocks_to_bits([blk]), start_index=7 << 40)
-    reps, t = 0, time.time()
-    while True:  # bounded sample: whole rounds of 16 SBOX until >= min_s of CPU work
-        if model == "1bit":
-            ok.sub_bytes_gal_mul(cts, threads)
-        else:
-            ok.sub_bytes8(cts, threads)
-        reps += 1
-        dt = time.time() - t
-        if dt >= min_s:
-            break
-    return {"value": reps / (10 * dt), "unit": "blocks/s", "cores": threads, "kind": "port",
-            "sample": f"{reps} x 16 SBOX " + ("8->24 circuit bootstraps" if model == "1bit" else
-                                              "bootstrap_with_lut (CBS-VP + extract_bits)")
-                      + " (one AES round of one block each) on "
-                      f"{threads} threads in {dt:.2f} s; blocks/s = rounds/s / 10"}
+    cts = ck.encrypt_bits_raw(aes_128.blocks_to_bits([blk]))  # fresh indices
+    if rk is None:
+        ek = b"".join(aes_128.key_schedule_plain(README_KEY))
+        rk = ck.encrypt_bits_raw([b for byte in ek for b in aes_128.u8_to_bits(byte)])
+    rounds = 10
+    t = time.time()
+    if model == "1bit":
+        out = ok.aes_encrypt_block(rk, cts, rounds, threads=threads)
+    else:
+        out = ok.aes8_encrypt_block(rk, cts, rounds, threads=threads)
+    dt = time.time() - t
+    correct = aes_128.bits_to_blocks(ck.decrypt_bits_raw(out))[0] == aes_128.encrypt_block_plain(
+        aes_128.key_schedule_plain(README_KEY), blk, rounds)
+    return {"value": 1.0 / dt, "unit": "blocks/s", "cores": threads, "kind": "port",
+            "nproc": os.cpu_count(), "cpu_share": cpu_share(), "correct": bool(correct),
+            "extrapolated_128_blocks_per_s": 1.0 / dt,
+            "sample": f"1 block x {rounds} rounds measured directly ({dt:.2f} s; 16 SBOX "
+                      + ("8->24 circuit bootstraps" if model == "1bit" else "bootstrap_with_lut") +
+                      f" per round on {threads} threads, oracle/tfhe_oracle.c); the 128-block figure is "
+                      "extrapolated (blocks independent, same cores)"}
+
+
+def model8_leg(torch, dev, nb, threads):
+    """BASELINE configs[4] (ShortintWoppbs8BitSboxPbsAesEncrypt, shortint_woppbs_8bit params) on a bounded
+    batch: nb counter blocks, one warm-up and one timed 10-round step, decrypted against plain AES."""
+    import tfhe_aes
+    from tfhe_aes import aes_128
+    from tfhe_aes import distributed as D
+    pid = tfhe_aes.PARAMS_WOPPBS_8BIT
+    t = time.time()
+    ck, raw = tfhe_aes.generate_keys_raw(pid, SEED, threads=threads)
+    ctx = tfhe_aes.context_from_raw(pid, raw, device=dev)
+    del raw
+    setup_s = time.time() - t
+    L = tfhe_aes.bit_len(pid)
+    E8 = aes_128.ShortintWoppbs8BitSboxPbsAesEncrypt
+    ek = b"".join(aes_128.key_schedule_plain(README_KEY))
+    rk = ck.encrypt_bits_raw([b for byte in ek for b in aes_128.u8_to_bits(byte)])
+    blocks = D.counter_blocks_for_rank(README_IV, 0, 1, nb)
+    cts = ck.encrypt_bits_raw(aes_128.blocks_to_bits(blocks))
+    rk_dev = torch.from_numpy(rk.view(np.int64)).to(f"cuda:{dev}")
+    blk_dev = torch.from_numpy(cts.view(np.int64)).to(f"cuda:{dev}")
+    out_dev = torch.empty_like(blk_dev)
+    torch.cuda.synchronize()
+    step = lambda: E8.encrypt_blocks_device(ctx, rk_dev.data_ptr(), blk_dev.data_ptr(), nb, 10, out_dev.data_ptr())
+    step()
+    ctx.synchronize()
+    t0 = time.time()
+    step()
+    ctx.synchronize()
+    dt = time.time() - t0
+    got = aes_128.bits_to_blocks(ck.decrypt_bits_raw(out_dev.cpu().numpy().view(np.uint64)))
+    ek_plain = aes_128.key_schedule_plain(README_KEY)
+    correct = all(g == aes_128.encrypt_block_plain(ek_plain, b, 10) for g, b in zip(got, blocks))
+    del ctx
+    return {"config": f"ShortintWoppbs8BitSboxPbsAesEncrypt, {nb} counter blocks x 10 rounds on 1 GPU "
+                      "(BASELINE configs[4]); 1 warm-up + 1 timed step", "blocks": nb, "s_per_step": dt,
+            "value": nb / dt, "unit": "blocks/s", "bit_len": L, "setup_s": setup_s, "correct": bool(correct)}
 
 
 if __name__ == "__main__":

@@ -111,7 +111,12 @@ int tae_context_params(const tae_context *ctx, tae_params *out);
 int tae_encrypt(const tae_client_key *ck, uint64_t bit, tae_bit **out);       /* ClientKey::encrypt */
 int tae_decrypt(const tae_client_key *ck, const tae_bit *bit, uint64_t *out); /* ClientKey::decrypt */
 int tae_trivial(const tae_context *ctx, uint64_t bit, tae_bit **out);         /* ContextT::trivial */
-/* raw: encrypt `count` bits with explicit encryption indices start..start+count ([count][K+1]) */
+/* raw: encrypt `count` bits ([count][K+1]) with encryption indices start..start+count-1.  Each index
+ * selects the ciphertext's mask and noise streams (DESIGN.md keygen spec), so an index must never be
+ * reused for a different plaintext under one key: explicit ranges must lie below 2^63 (TAE_E_ARG
+ * otherwise); start_index = TAE_INDEX_AUTO reserves `count` fresh indices from the key's counter,
+ * the region tae_encrypt draws from (disjoint from every explicit range). */
+#define TAE_INDEX_AUTO UINT64_MAX
 int tae_encrypt_bits_raw(const tae_client_key *ck, const uint8_t *bits, size_t count,
                          uint64_t start_index, uint64_t *out);
 int tae_decrypt_bits_raw(const tae_client_key *ck, const uint64_t *cts, size_t count, uint8_t *bits);
@@ -129,12 +134,26 @@ int tae_bit_noise_level(const tae_bit *bit, uint64_t *noise_level_squared);
 int tae_bit_data(const tae_bit *bit, uint64_t *out, size_t len); /* LWE coefficients [K+1] */
 int tae_bit_from_data(const tae_context *ctx, const uint64_t *data, size_t len,
                       uint64_t noise_level_squared, tae_bit **out); /* BitCt::with_noise_level */
+/* BitXorAssign over whole arrays of bits (xor_state, src/aes_128/fhe/data_model.rs:270-274):
+ * lhs[i] += rhs[i] (wrapping u64 LWE addition = XOR of the encoded bits) for `count` bit ciphertexts
+ * of tae_bit_len words each, on the context's GPU.  With both noise arrays (squared noise levels per
+ * bit) the reference's NoiseTooBig rule is enforced before anything is written and out_noise_sq
+ * (may be NULL) receives the sums; the component-independence check needs BitCt handles
+ * (tae_bit_xor_assign) and is the caller's duty here. */
+int tae_xor_batch(const tae_context *ctx, uint64_t *lhs, const uint64_t *rhs, size_t count,
+                  const uint64_t *lhs_noise_sq, const uint64_t *rhs_noise_sq, uint64_t *out_noise_sq, int mem);
 
 /* ---- LUT + circuit bootstrap (shortint_woppbs_1bit.rs:274-336) ----------------------------- */
 /* generate_lookup_table: f_values[1 << input_bits] */
 int tae_generate_lookup_table(const tae_context *ctx, int input_bits, int output_bits,
                               const uint64_t *f_values, tae_lut **out);
 void tae_lut_free(tae_lut *lut);
+/* generate_multivariate_luts (shortint_woppbs_1bit.rs:366-403) without a context, for any power-of-two
+ * polynomial size: out [output_bits][poly_size << max(0, input_bits - log2 poly_size)], small LUT j
+ * holding encode_bit(bit output_bits-1-j of f(v)) at coefficient v (the layout pinned by the
+ * reference's tests :665-697); out_len must equal that size. */
+int tae_generate_multivariate_luts(int poly_size, int input_bits, int output_bits, const uint64_t *f_values,
+                                   uint64_t *out, size_t out_len);
 int tae_lut_data(const tae_lut *lut, uint64_t *out, size_t len, size_t *needed);
 /* FheContext::circuit_bootstrap(&[&BitCt], &WopbsLUTBase) -> Vec<BitCt> */
 int tae_circuit_bootstrap(const tae_context *ctx, const tae_bit *const *bits, size_t n_bits,
@@ -191,6 +210,9 @@ int tae_set_timing(const tae_context *ctx, int on);
 int tae_last_stage_times(const tae_context *ctx, float *ms5);
 /* [keyswitch, pbs, pfks, ggsw_fft, vp, extract_bits, linear] ms + the CBS-level PBS launch count */
 int tae_last_stage_times_v2(const tae_context *ctx, float *ms8);
+/* v2's eight values, then the ms and the ciphertext count of the throughput blind-rotation kernel's
+ * own launches (br512x4, without the small-batch remainder) -- the roofline's launch duration */
+int tae_last_stage_times_v3(const tae_context *ctx, double *v10);
 
 #ifdef __cplusplus
 }

@@ -447,13 +447,18 @@ void or_fft_add_bwd_torus(const or_fft *f, const or_c64 *in, uint64_t *out) {
 /* ======================================================================================
  * GLWE / LWE encryption (tfhe-rs encrypt_lwe_ciphertext / encrypt_glwe_ciphertext), with
  * the keygen randomness spec of DESIGN.md: ciphertext #idx of purpose P draws its mask from
- * ChaCha20(seed, nonce=2P, ctr=idx*2^24) and its noise from ChaCha20(seed, nonce=2P+1, same ctr).
+ * ChaCha20(seed, nonce = 2P | (idx >> 40) << 8, ctr = (idx mod 2^40) * 2^24) and its noise from
+ * the same stream origin with nonce 2P+1 (injective over 64-bit indices).
  * ====================================================================================== */
+static uint64_t ct_nonce(int purpose, int noise, uint64_t idx) {
+    return (2ull * (uint64_t)purpose + (uint64_t)noise) | ((idx >> 40) << 8);
+}
+static uint64_t ct_counter(uint64_t idx) { return (idx & ((1ull << 40) - 1)) * CT_STRIDE; }
 static void lwe_encrypt(const uint64_t *sk, int dim, uint64_t msg, double sigma, const uint8_t seed[32],
                         int purpose, uint64_t idx, uint64_t *out) {
     rng_t rm, rn;
-    rng_init(&rm, seed, 2ull * purpose, idx * CT_STRIDE);
-    rng_init(&rn, seed, 2ull * purpose + 1, idx * CT_STRIDE);
+    rng_init(&rm, seed, ct_nonce(purpose, 0, idx), ct_counter(idx));
+    rng_init(&rn, seed, ct_nonce(purpose, 1, idx), ct_counter(idx));
     uint64_t b = 0;
     for (int i = 0; i < dim; i++) {
         out[i] = rng_u64(&rm);
@@ -467,8 +472,8 @@ static void lwe_encrypt(const uint64_t *sk, int dim, uint64_t msg, double sigma,
 static void glwe_encrypt(const uint64_t *S, int k, int N, const uint64_t *msg, double sigma,
                          const uint8_t seed[32], int purpose, uint64_t idx, uint64_t *out) {
     rng_t rm, rn;
-    rng_init(&rm, seed, 2ull * purpose, idx * CT_STRIDE);
-    rng_init(&rn, seed, 2ull * purpose + 1, idx * CT_STRIDE);
+    rng_init(&rm, seed, ct_nonce(purpose, 0, idx), ct_counter(idx));
+    rng_init(&rn, seed, ct_nonce(purpose, 1, idx), ct_counter(idx));
     uint64_t *B = out + (size_t)k * N;
     for (int p = 0; p < k; p++)
         for (int j = 0; j < N; j++) out[(size_t)p * N + j] = rng_u64(&rm);

@@ -41,6 +41,66 @@ def test_encrypt_matches_oracle_and_decrypts(product_raw, oracle_keys):
     assert list(oracle_keys.decrypt_bits(cts)) == bits
 
 
+def test_encryption_indices_never_alias(product_raw, oracle_keys):
+    """Ciphertext #idx draws its mask / noise from ChaCha20(nonce 2P | (idx >> 40) << 8, counter
+    (idx mod 2^40) 2^24): indices 2^40 apart no longer share a stream (the counter alone wraps), and
+    the oracle restates the same rule."""
+    ck, _ = product_raw
+    from tests.conftest import SEED
+    for i in (0, 5, 1000):
+        a = ck.encrypt_bits_raw([0], start_index=i)
+        b = ck.encrypt_bits_raw([0], start_index=i + (1 << 40))
+        c = ck.encrypt_bits_raw([0], start_index=i + (7 << 40))
+        assert not np.array_equal(a[0, :64], b[0, :64]) and not np.array_equal(a[0, :64], c[0, :64])
+        assert np.array_equal(b, oracle_keys.encrypt_bits([0], SEED, i + (1 << 40)))
+    masks = np.stack([ck.encrypt_bits_raw([0], start_index=s)[0, :8] for s in range(0, 1 << 44, 1 << 40)])
+    assert len({m.tobytes() for m in masks}) == len(masks)
+
+
+def test_encryption_index_ranges(product_raw):
+    """Explicit raw indices stay below 2^63; TAE_INDEX_AUTO (start_index=None) reserves fresh ones
+    from the key's counter, the region tae_encrypt uses, so auto ranges never repeat."""
+    ck, _ = product_raw
+    with pytest.raises(tfhe_aes.TaeError):
+        ck.encrypt_bits_raw([0], start_index=1 << 63)
+    with pytest.raises(tfhe_aes.TaeError):
+        ck.encrypt_bits_raw([0, 1], start_index=(1 << 63) - 1)
+    a, b = ck.encrypt_bits_raw([1, 0, 1]), ck.encrypt_bits_raw([1, 0, 1])
+    assert not np.array_equal(a[:, :-1], b[:, :-1])
+    assert list(ck.decrypt_bits_raw(a)) == [1, 0, 1] == list(ck.decrypt_bits_raw(b))
+
+
+def test_context_from_raw_checks_key_arrays(product_raw):
+    """Short, mistyped or wrongly sized key arrays are refused before any pointer reaches C."""
+    _, (ksk, bsk, pfpksk) = product_raw
+    with pytest.raises(ValueError):
+        tfhe_aes.context_from_raw(tfhe_aes.PARAMS_SQRD_LVL_64, (ksk[:-1], bsk, pfpksk))
+    with pytest.raises(ValueError):
+        tfhe_aes.context_from_raw(tfhe_aes.PARAMS_SQRD_LVL_64, (ksk.astype(np.float64), bsk, pfpksk))
+    with pytest.raises(ValueError):
+        tfhe_aes.save_keys("/tmp/never-written.taekey", tfhe_aes.PARAMS_SQRD_LVL_64, None, (ksk, bsk[:10], pfpksk))
+
+
+def test_product_lut_generator_exact_layout(golden, oracle_mod):
+    """The product's context-free generate_multivariate_luts (tae_generate_multivariate_luts) against
+    the reference's exact arrays (shortint_woppbs_1bit.rs:665-697): N=16 3 -> 2 (one polynomial per
+    output) and N=8 5 -> 2 (multi-polynomial: 4 polynomials per output), and equal to the oracle on
+    the AES LUTs."""
+    lut = tfhe_aes.generate_multivariate_luts(16, 3, 2, lambda v: v)
+    assert lut.size == 16 * 2
+    for j, exp in enumerate(golden["lut_vertical_packing_3_2_16"]):
+        assert list(lut[16 * j:16 * (j + 1)]) == [b << 63 for b in exp]
+    lut = tfhe_aes.generate_multivariate_luts(8, 5, 2, lambda v: v)
+    assert lut.size == 8 * 4 * 2
+    for j, exp in enumerate(golden["lut_multipoly_5_2_8"]):
+        assert list(lut[32 * j:32 * (j + 1)]) == [b << 63 for b in exp]
+    f = lambda x: (aes_128.gf_256_mul(aes_128.SBOX[x], 1) << 16) | (aes_128.gf_256_mul(aes_128.SBOX[x], 2) << 8) | \
+        aes_128.gf_256_mul(aes_128.SBOX[x], 3)
+    assert np.array_equal(tfhe_aes.generate_multivariate_luts(512, 8, 24, f), oracle_mod.generate_lut(512, 8, 24, f))
+    with pytest.raises(tfhe_aes.TaeError):
+        tfhe_aes.generate_multivariate_luts(12, 3, 2, lambda v: v)  # not a power of two
+
+
 def test_bit_encrypt_decrypt(product_raw):
     ck, _ = product_raw
     b1 = ck.encrypt(Cleartext(0))

@@ -1,0 +1,74 @@
+"""The metric's own shapes on the GPU (BASELINE configs[2]) and the multi-rank device path.
+
+- 128 counter-mode blocks in one batched call: every CBS launch is 128 x 16 x 8 = 16384 PBS, so
+  Engine::bootstrap runs 21 whole rounds of br512x4 (16128 ciphertexts) plus a 256-ciphertext
+  br512lat remainder, and vertical packing covers 128 x 16 x 24 outputs.  2 rounds keep it cheap
+  (reduced-round semantics of plain.rs:75-103: ARK(rk0), one full round, final round with rk10).
+  All 128 blocks decrypt to plain AES; the first block, the first block past the br512x4 /
+  br512lat split (block 126: PBS index 16128) and the last equal the oracle word for word.
+- A context built from device-resident server keys (tae_context_create_raw with TAE_MEM_DEVICE,
+  what every rank > 0 of bench.py runs after the RCCL broadcast) computes the same ciphertexts as
+  the host-built one, with device-resident inputs and outputs as well.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import tfhe_aes
+from tfhe_aes import _native as N
+from tfhe_aes import aes_128
+
+pytestmark = pytest.mark.gpu
+
+BIG = 4 * 512 + 1
+E = aes_128.ShortintWoppbs1BitSboxGalMulPbsAesEncrypt
+
+
+@pytest.fixture(scope="module")
+def client(product_raw):
+    return product_raw[0]
+
+
+@pytest.fixture(scope="module")
+def readme_setup(client, golden):
+    g = golden["readme_ctr"]
+    key, iv = bytes.fromhex(g["key"]), bytes.fromhex(g["iv"])
+    ek = b"".join(aes_128.key_schedule_plain(key))
+    rk = client.encrypt_bits_raw([b for byte in ek for b in aes_128.u8_to_bits(byte)], start_index=300_000)
+    return key, iv, rk
+
+
+def test_full_batch_128_blocks_two_rounds(gpu_context, oracle_keys, client, readme_setup):
+    key, iv, rk = readme_setup
+    nb = 128
+    blocks = aes_128.counter_blocks(iv, nb)
+    cts = client.encrypt_bits_raw(aes_128.blocks_to_bits(blocks), start_index=400_000).reshape(nb, 128, BIG)
+    out = E.encrypt_blocks_raw(gpu_context, rk, cts, rounds=2)
+    got = aes_128.bits_to_blocks(client.decrypt_bits_raw(out))
+    assert got == aes_128.expand_key_and_encrypt_blocks(key, blocks, 2)
+    # 16384 PBS per launch = 21 x 768 (br512x4) + 256 (br512lat): block 126 starts the remainder
+    for b in (0, 126, nb - 1):
+        ref = oracle_keys.aes_encrypt_block(rk, cts[b], 2, threads=16)
+        assert np.array_equal(out[b], ref), b
+
+
+def test_device_key_context_matches_host_context(gpu_context, product_raw, client, readme_setup):
+    torch = pytest.importorskip("torch")
+    _, keys = product_raw
+    dev = [torch.from_numpy(k.view(np.int64)).to("cuda:0") for k in keys]
+    ctx_d = tfhe_aes.context_from_raw(tfhe_aes.PARAMS_SQRD_LVL_64, [t.data_ptr() for t in dev], device=0,
+                                      mem=N.TAE_MEM_DEVICE)
+    key, iv, rk = readme_setup
+    blocks = aes_128.counter_blocks(iv, 3)
+    cts = client.encrypt_bits_raw(aes_128.blocks_to_bits(blocks), start_index=500_000).reshape(3, 128, BIG)
+    ref = E.encrypt_blocks_raw(gpu_context, rk, cts, rounds=1)
+    assert np.array_equal(E.encrypt_blocks_raw(ctx_d, rk, cts, rounds=1), ref)
+    # device-resident rk / blocks / output, written on torch's stream right before the call
+    d_rk = torch.from_numpy(rk.view(np.int64)).to("cuda:0", non_blocking=True)
+    d_in = torch.from_numpy(cts.view(np.int64)).to("cuda:0", non_blocking=True)
+    d_out = torch.full_like(d_in, -1)
+    E.encrypt_blocks_device(ctx_d, d_rk.data_ptr(), d_in.data_ptr(), 3, 1, d_out.data_ptr())
+    assert np.array_equal(d_out.cpu().numpy().view(np.uint64), ref)
+    assert aes_128.bits_to_blocks(client.decrypt_bits_raw(ref)) == aes_128.expand_key_and_encrypt_blocks(key, blocks, 1)
+    del ctx_d  # the context borrows the key buffers: free it first

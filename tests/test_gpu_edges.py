@@ -74,3 +74,21 @@ def test_argument_errors(gpu_context, client):
     with pytest.raises(tfhe_aes.TaeError) as e:
         tfhe_aes.get_params(99)
     assert e.value.code == N.TAE_E_PARAM
+
+
+def test_xor_batch_state(gpu_context, client):
+    """tae_xor_batch = xor_state (data_model.rs:270-274) over a whole 128-bit state: decrypts to the
+    XOR, noise levels add, and NoiseTooBig (max noise^2 64 at lvl_64) is raised before any write."""
+    rng = np.random.default_rng(3)
+    a_bits, b_bits = rng.integers(0, 2, 128), rng.integers(0, 2, 128)
+    a = client.encrypt_bits_raw(a_bits, start_index=900_000)
+    b = client.encrypt_bits_raw(b_bits, start_index=901_000)
+    ref = (a + b).copy()
+    lvl = gpu_context.xor_batch(a, b, np.full(128, 9, np.uint64), np.ones(128, np.uint64))
+    assert np.array_equal(a, ref)
+    assert list(lvl) == [10] * 128
+    assert list(client.decrypt_bits_raw(a)) == list(a_bits ^ b_bits)
+    before = a.copy()
+    with pytest.raises(tfhe_aes.NoiseTooBig):
+        gpu_context.xor_batch(a, b, np.full(128, 60, np.uint64), np.full(128, 5, np.uint64))
+    assert np.array_equal(a, before)

@@ -15,7 +15,6 @@
 // Engine::bootstrap picks by batch size.
 #pragma once
 #include "br512.hpp"
-#include "br512x2.hpp"
 #include "br512x4.hpp"
 
 namespace tae {
@@ -28,8 +27,8 @@ using br512::M;
 using br512::N;
 using br512::pidx;
 using br512::u32x4;
-using br512x2::mac_pos;
-using br512x2::wave_sync;
+using br512::mac_pos;
+using br512::wave_sync;
 using br512x4::dft16x4;
 
 constexpr int THREADS = 1024;

@@ -16,7 +16,6 @@
 // each LDS access of a wave touches 64 consecutive coefficients.
 #pragma once
 #include "br512.hpp"
-#include "br512x2.hpp"
 
 namespace tae {
 namespace br512x4 {
@@ -28,10 +27,9 @@ using br512::M;
 using br512::N;
 using br512::pidx;
 using br512::u32x4;
-using br512::W16;
-using br512x2::mac_pos;
-using br512x2::swap16;
-using br512x2::wave_sync;
+using br512::mac_pos;
+using br512::swap16;
+using br512::wave_sync;
 
 constexpr int C = 3, JOBS = C * K1, THREADS = 1024;
 
@@ -39,6 +37,7 @@ constexpr int C = 3, JOBS = C * K1, THREADS = 1024;
 // it completes parts of the phase, so the SIMD arbiter favours the waves that are behind and the
 // four waves of a SIMD reach the next barrier together (oldest-first arbitration otherwise starves
 // the youngest wave, whose tail then runs alone with its latencies exposed).
+#define DBG_SYNC() br512::lds_sync()
 #ifndef TAE_X4_NORR
 #define PRIO(n) __builtin_amdgcn_s_setprio(n)
 #else

@@ -83,15 +83,30 @@ std::vector<const tae::BitCt *> unwrap(const tae_bit *const *bits, size_t n) {
     return v;
 }
 
-// run `fn(d_in, d_out)` with host staging when mem == TAE_MEM_HOST
+// run `fn(d_in, d_out, d_aux)` with host staging when mem == TAE_MEM_HOST.  `aux` (aux_bytes, may
+// be null) is a second input in the same memory kind, staged the same way (a LUT).
 template <class TI, class TO, class F>
-void staged(tae_context const *ctx, const TI *in, size_t in_bytes, TO *out, size_t out_bytes, int mem, F fn) {
+void staged(tae_context const *ctx, const TI *in, size_t in_bytes, TO *out, size_t out_bytes, int mem, F fn,
+            const uint64_t *aux = nullptr, size_t aux_bytes = 0) {
     tae::Context &c = *ctx->ctx;
     std::lock_guard<std::mutex> g(c.mutex());
     tae::Engine &e = c.engine();
     tae::hip_check(hipSetDevice(e.device()), "hipSetDevice");
+    struct Dev {
+        void *p = nullptr;
+        ~Dev() {
+            if (p) hipFree(p);
+        }
+    } daux;
+    if (aux && mem != TAE_MEM_DEVICE) {
+        tae::hip_check(hipMalloc(&daux.p, std::max<size_t>(aux_bytes, 16)), "hipMalloc");
+        tae::hip_check(hipMemcpyAsync(daux.p, aux, aux_bytes, hipMemcpyHostToDevice, e.stream()), "upload aux");
+        aux = static_cast<const uint64_t *>(daux.p);
+    }
+    auto call = [&](const TI *a, TO *b) { fn(a, b, aux); };
     if (mem == TAE_MEM_DEVICE) {
-        fn(in, out);
+        e.order_after_caller();
+        call(in, out);
         e.synchronize();
         return;
     }
@@ -102,11 +117,11 @@ void staged(tae_context const *ctx, const TI *in, size_t in_bytes, TO *out, size
         throw tae::HipError{"hipMalloc"};
     }
     try {
-        tae::hip_check(hipMemcpy(di, in, in_bytes, hipMemcpyHostToDevice), "upload");
-        tae::hip_check(hipMemset(dout, 0, out_bytes), "memset");
-        fn(static_cast<const TI *>(di), static_cast<TO *>(dout));
+        // everything on the engine stream, in order (the kernels overwrite every output word)
+        tae::hip_check(hipMemcpyAsync(di, in, in_bytes, hipMemcpyHostToDevice, e.stream()), "upload");
+        call(static_cast<const TI *>(di), static_cast<TO *>(dout));
+        tae::hip_check(hipMemcpyAsync(out, dout, out_bytes, hipMemcpyDeviceToHost, e.stream()), "download");
         e.synchronize();
-        tae::hip_check(hipMemcpy(out, dout, out_bytes, hipMemcpyDeviceToHost), "download");
     } catch (...) {
         hipFree(di);
         hipFree(dout);
@@ -291,7 +306,7 @@ int tae_encrypt(const tae_client_key *ck, uint64_t bit, tae_bit **out) {
         auto &c = const_cast<tae_client_key *>(ck)->ck;
         auto b = std::make_unique<tae_bit>();
         b->b.ct.assign(c.bit_len(), 0);
-        c.encrypt_model_bit_at(bit, c.next_index.fetch_add(1), b->b.ct.data());
+        c.encrypt_model_bit_at(bit, tae::kAutoIndexBase + c.next_index.fetch_add(1), b->b.ct.data());
         // BitCt::fresh (1-bit model: noise^2 1 + a new component id; 8-bit: NoiseLevel::NOMINAL)
         b->b.noise = c.p.model == 8 ? tae::NoiseLevel{1, {}} : tae::NoiseLevel::with_noise_level(1, tae::next_ct_id());
         b->b.max_noise_sq = c.p.max_noise_sq;
@@ -314,15 +329,23 @@ int tae_trivial(const tae_context *ctx, uint64_t bit, tae_bit **out) {
     });
 }
 
+// Resolve the encryption indices of a raw call: TAE_INDEX_AUTO reserves `count` fresh indices from
+// the key's counter (the region tae_encrypt uses); an explicit range must lie below kAutoIndexBase.
+static uint64_t raw_index_range(const tae_client_key *ck, size_t count, uint64_t start_index) {
+    if (start_index == TAE_INDEX_AUTO) return tae::kAutoIndexBase + const_cast<tae_client_key *>(ck)->ck.next_index.fetch_add(count);
+    require(start_index < tae::kAutoIndexBase && count <= tae::kAutoIndexBase - start_index,
+            "explicit encryption indices must lie below 2^63 (use TAE_INDEX_AUTO for fresh ones)");
+    return start_index;
+}
+
 int tae_encrypt_bits_raw(const tae_client_key *ck, const uint8_t *bits, size_t count, uint64_t start_index,
                          uint64_t *out) {
     return guarded([&] {
         require(ck && (bits || !count) && (out || !count), "null");
+        for (size_t i = 0; i < count; i++) require(bits[i] < 2, "cleartext out of bounds");
+        const uint64_t first = raw_index_range(ck, count, start_index);
         const size_t L = ck->ck.bit_len();
-        for (size_t i = 0; i < count; i++) {
-            require(bits[i] < 2, "cleartext out of bounds");
-            ck->ck.encrypt_model_bit_at(bits[i], start_index + i, out + i * L);
-        }
+        for (size_t i = 0; i < count; i++) ck->ck.encrypt_model_bit_at(bits[i], first + i, out + i * L);
     });
 }
 
@@ -330,8 +353,9 @@ int tae_encrypt_ints_raw(const tae_client_key *ck, const uint8_t *values, size_t
                          uint64_t *out) {
     return guarded([&] {
         require(ck && (values || !count) && (out || !count), "null");
+        const uint64_t first = raw_index_range(ck, count, start_index);
         const size_t L = ck->ck.p.big_len();
-        for (size_t i = 0; i < count; i++) ck->ck.encrypt_int_at(values[i], start_index + i, out + i * L);
+        for (size_t i = 0; i < count; i++) ck->ck.encrypt_int_at(values[i], first + i, out + i * L);
     });
 }
 
@@ -399,6 +423,72 @@ int tae_generate_lookup_table(const tae_context *ctx, int input_bits, int output
 }
 
 void tae_lut_free(tae_lut *lut) { delete lut; }
+
+int tae_generate_multivariate_luts(int poly_size, int input_bits, int output_bits, const uint64_t *f_values,
+                                   uint64_t *out, size_t out_len) {
+    return guarded([&] {
+        require(f_values && out, "null");
+        require(poly_size >= 2 && (poly_size & (poly_size - 1)) == 0 && poly_size <= (1 << 16),
+                "polynomial size must be a power of two");
+        require(input_bits >= 1 && input_bits <= 24 && output_bits >= 1 && output_bits <= 64, "bit counts out of range");
+        require(out_len == tae::lut_small_len(poly_size, input_bits) * (size_t)output_bits, "length mismatch");
+        tae::generate_lut(poly_size, input_bits, output_bits, f_values, out);
+    });
+}
+
+int tae_xor_batch(const tae_context *ctx, uint64_t *lhs, const uint64_t *rhs, size_t count,
+                  const uint64_t *lhs_noise_sq, const uint64_t *rhs_noise_sq, uint64_t *out_noise_sq, int mem) {
+    return guarded([&] {
+        require(ctx && (lhs || !count) && (rhs || !count), "null");
+        require((lhs_noise_sq == nullptr) == (rhs_noise_sq == nullptr), "give both noise arrays or neither");
+        const uint64_t max_sq = ctx->ctx->params().max_noise_sq;
+        if (lhs_noise_sq) {
+            // BitXorAssign's noise rule (shortint_woppbs_1bit.rs:134-142, NoiseLevelWithComponents::add
+            // + MaxNoiseLevel::validate): squared noise levels add and must stay <= max_noise_level^2
+            for (size_t i = 0; i < count; i++) {
+                const uint64_t s = lhs_noise_sq[i] + rhs_noise_sq[i];
+                if (s > max_sq)
+                    throw tae::ModelError{TAE_E_NOISE, "NoiseTooBig: noise level squared " + std::to_string(s) +
+                                                           " above " + std::to_string(max_sq) + " at element " +
+                                                           std::to_string(i)};
+            }
+        }
+        const size_t words = count * ctx->ctx->bit_len();
+        if (count) {
+            tae::Context &c = *ctx->ctx;
+            std::lock_guard<std::mutex> g(c.mutex());
+            tae::Engine &e = c.engine();
+            tae::hip_check(hipSetDevice(e.device()), "hipSetDevice");
+            if (mem == TAE_MEM_DEVICE) {
+                e.order_after_caller();
+                e.lwe_add(lhs, rhs, words);
+                e.synchronize();
+            } else {
+                void *da = nullptr, *db = nullptr;
+                tae::hip_check(hipMalloc(&da, words * 8), "hipMalloc");
+                if (hipMalloc(&db, words * 8) != hipSuccess) {
+                    hipFree(da);
+                    throw tae::HipError{"hipMalloc"};
+                }
+                try {
+                    tae::hip_check(hipMemcpyAsync(da, lhs, words * 8, hipMemcpyHostToDevice, e.stream()), "upload");
+                    tae::hip_check(hipMemcpyAsync(db, rhs, words * 8, hipMemcpyHostToDevice, e.stream()), "upload");
+                    e.lwe_add(static_cast<uint64_t *>(da), static_cast<const uint64_t *>(db), words);
+                    tae::hip_check(hipMemcpyAsync(lhs, da, words * 8, hipMemcpyDeviceToHost, e.stream()), "download");
+                    e.synchronize();
+                } catch (...) {
+                    hipFree(da);
+                    hipFree(db);
+                    throw;
+                }
+                hipFree(da);
+                hipFree(db);
+            }
+        }
+        if (out_noise_sq && lhs_noise_sq)
+            for (size_t i = 0; i < count; i++) out_noise_sq[i] = lhs_noise_sq[i] + rhs_noise_sq[i];
+    });
+}
 
 int tae_lut_data(const tae_lut *lut, uint64_t *out, size_t len, size_t *needed) {
     return guarded([&] {
@@ -488,7 +578,7 @@ int tae_stage_keyswitch(const tae_context *ctx, const uint64_t *in, size_t count
         require(ctx && in && out, "null");
         const auto &p = ctx->ctx->params();
         staged(ctx, in, count * p.big_len() * 8, out, count * p.small_len() * 8, mem,
-               [&](const uint64_t *a, uint64_t *b) { ctx->ctx->engine().keyswitch(a, b, count); });
+               [&](const uint64_t *a, uint64_t *b, const uint64_t *) { ctx->ctx->engine().keyswitch(a, b, count); });
     });
 }
 
@@ -499,7 +589,7 @@ int tae_stage_pbs_shift_boolean(const tae_context *ctx, const uint64_t *small, s
         const auto &p = ctx->ctx->params();
         require(level >= 1 && level <= p.cbs_l, "level out of range");
         staged(ctx, small, count * p.small_len() * 8, big, count * p.big_len() * 8, mem,
-               [&](const uint64_t *a, uint64_t *b) { ctx->ctx->engine().pbs_shift_boolean(a, b, count, level); });
+               [&](const uint64_t *a, uint64_t *b, const uint64_t *) { ctx->ctx->engine().pbs_shift_boolean(a, b, count, level); });
     });
 }
 
@@ -508,21 +598,10 @@ int tae_stage_bootstrap(const tae_context *ctx, const uint64_t *small, size_t co
     return guarded([&] {
         require(ctx && small && lut_glwe && big, "null");
         const auto &p = ctx->ctx->params();
-        void *d_lut = nullptr;
-        const uint64_t *lut = lut_glwe;
-        if (mem != TAE_MEM_DEVICE) {
-            tae::hip_check(hipMalloc(&d_lut, p.glwe_len() * 8), "hipMalloc");
-            tae::hip_check(hipMemcpy(d_lut, lut_glwe, p.glwe_len() * 8, hipMemcpyHostToDevice), "upload");
-            lut = static_cast<const uint64_t *>(d_lut);
-        }
-        try {
-            staged(ctx, small, count * p.small_len() * 8, big, count * p.big_len() * 8, mem,
-                   [&](const uint64_t *a, uint64_t *b) { ctx->ctx->engine().bootstrap(a, lut, b, count, 0, 0); });
-        } catch (...) {
-            if (d_lut) hipFree(d_lut);
-            throw;
-        }
-        if (d_lut) hipFree(d_lut);
+        staged(
+            ctx, small, count * p.small_len() * 8, big, count * p.big_len() * 8, mem,
+            [&](const uint64_t *a, uint64_t *b, const uint64_t *lut) { ctx->ctx->engine().bootstrap(a, lut, b, count, 0, 0); },
+            lut_glwe, p.glwe_len() * 8);
     });
 }
 
@@ -532,7 +611,7 @@ int tae_stage_pfks_ggsw(const tae_context *ctx, const uint64_t *big, size_t coun
         const auto &p = ctx->ctx->params();
         require(level >= 1 && level <= p.cbs_l, "level out of range");
         staged(ctx, big, count * p.big_len() * 8, ggsw, count * p.cbs_ggsw_len() * 8, mem,
-               [&](const uint64_t *a, uint64_t *b) { ctx->ctx->engine().pfks_into_ggsw(a, b, count, level); });
+               [&](const uint64_t *a, uint64_t *b, const uint64_t *) { ctx->ctx->engine().pfks_into_ggsw(a, b, count, level); });
     });
 }
 
@@ -541,7 +620,7 @@ int tae_stage_ggsw_fourier(const tae_context *ctx, const uint64_t *ggsw, size_t 
         require(ctx && ggsw && ggsw_f, "null");
         const auto &p = ctx->ctx->params();
         staged(ctx, ggsw, count * p.cbs_ggsw_len() * 8, ggsw_f, count * p.cbs_ggsw_fourier_len() * 16, mem,
-               [&](const uint64_t *a, double *b) {
+               [&](const uint64_t *a, double *b, const uint64_t *) {
                    ctx->ctx->engine().ggsw_to_fourier(a, reinterpret_cast<tae::cplx *>(b), count);
                });
     });
@@ -552,24 +631,12 @@ int tae_stage_vertical_packing(const tae_context *ctx, const double *ggsw_f, siz
     return guarded([&] {
         require(ctx && ggsw_f && lut && out, "null");
         const auto &p = ctx->ctx->params();
-        void *d_lut = nullptr;
-        const uint64_t *l = lut;
-        if (mem != TAE_MEM_DEVICE) {
-            tae::hip_check(hipMalloc(&d_lut, (size_t)n_out * p.N * 8), "hipMalloc");
-            tae::hip_check(hipMemcpy(d_lut, lut, (size_t)n_out * p.N * 8, hipMemcpyHostToDevice), "upload");
-            l = static_cast<const uint64_t *>(d_lut);
-        }
-        try {
-            staged(ctx, ggsw_f, groups * n_in * p.cbs_ggsw_fourier_len() * 16, out, groups * n_out * p.big_len() * 8,
-                   mem, [&](const double *a, uint64_t *b) {
-                       ctx->ctx->engine().vertical_packing(reinterpret_cast<const tae::cplx *>(a), groups, n_in, l,
-                                                           n_out, b);
-                   });
-        } catch (...) {
-            if (d_lut) hipFree(d_lut);
-            throw;
-        }
-        if (d_lut) hipFree(d_lut);
+        staged(
+            ctx, ggsw_f, groups * n_in * p.cbs_ggsw_fourier_len() * 16, out, groups * n_out * p.big_len() * 8, mem,
+            [&](const double *a, uint64_t *b, const uint64_t *l) {
+                ctx->ctx->engine().vertical_packing(reinterpret_cast<const tae::cplx *>(a), groups, n_in, l, n_out, b);
+            },
+            lut, (size_t)n_out * p.N * 8);
     });
 }
 
@@ -594,6 +661,16 @@ int tae_last_stage_times_v2(const tae_context *ctx, float *ms8) {
         const float v[8] = {t.keyswitch, t.pbs, t.pfks, t.ggsw_fft, t.vertical_packing, t.extract, t.linear,
                             (float)t.pbs_launches};
         for (int i = 0; i < 8; i++) ms8[i] = v[i];
+    });
+}
+
+int tae_last_stage_times_v3(const tae_context *ctx, double *v10) {
+    return guarded([&] {
+        require(ctx && v10, "null");
+        const auto &t = ctx->ctx->engine().last_times();
+        const double v[10] = {t.keyswitch, t.pbs,    t.pfks,         t.ggsw_fft, t.vertical_packing,
+                              t.extract,   t.linear, (double)t.pbs_launches, t.pbs_main, t.pbs_main_cts};
+        for (int i = 0; i < 10; i++) v10[i] = v[i];
     });
 }
 

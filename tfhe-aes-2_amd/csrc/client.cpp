@@ -79,8 +79,8 @@ namespace {
 // LWE encryption of `msg` under key `sk` (dimension dim), ciphertext #idx of `purpose`.
 void lwe_encrypt(const uint8_t seed[32], Purpose purpose, uint64_t idx, const uint64_t *sk, int dim,
                  uint64_t msg, double sigma, uint64_t *out) {
-    ChaChaStream mask(seed, 2 * (uint64_t)purpose, idx * kCtStride);
-    ChaChaStream noise(seed, 2 * (uint64_t)purpose + 1, idx * kCtStride);
+    ChaChaStream mask(seed, ct_nonce(purpose, 0, idx), ct_counter(idx));
+    ChaChaStream noise(seed, ct_nonce(purpose, 1, idx), ct_counter(idx));
     uint64_t body = 0;
     for (int i = 0; i < dim; i++) {
         out[i] = mask.next_u64();
@@ -92,8 +92,8 @@ void lwe_encrypt(const uint8_t seed[32], Purpose purpose, uint64_t idx, const ui
 // GLWE encryption of plaintext polynomial `msg` (nullptr = 0) under the binary key S (k polys).
 void glwe_encrypt(const uint8_t seed[32], Purpose purpose, uint64_t idx, const uint64_t *S, int k,
                   int N, const uint64_t *msg, double sigma, uint64_t *out) {
-    ChaChaStream mask(seed, 2 * (uint64_t)purpose, idx * kCtStride);
-    ChaChaStream noise(seed, 2 * (uint64_t)purpose + 1, idx * kCtStride);
+    ChaChaStream mask(seed, ct_nonce(purpose, 0, idx), ct_counter(idx));
+    ChaChaStream noise(seed, ct_nonce(purpose, 1, idx), ct_counter(idx));
     const size_t kN = (size_t)k * N;
     for (size_t t = 0; t < kN; t++) out[t] = mask.next_u64();
     uint64_t *body = out + kN;

@@ -37,6 +37,17 @@ class ChaChaStream {
 // Keygen stream purposes (DESIGN.md keygen spec).
 enum Purpose : uint64_t { LWE_SK = 1, GLWE_SK = 2, KSK = 3, BSK = 4, PFPKSK = 5, ENCRYPT = 6, ENCRYPT_INT = 7 };
 constexpr uint64_t kCtStride = 1ull << 24;
+// Ciphertext #idx of purpose P starts its mask stream at ChaCha20(nonce = 2P | (idx >> 40) << 8,
+// counter = (idx mod 2^40) * 2^24) and its noise stream at nonce 2P + 1 (same high bits, same counter):
+// injective over all 64-bit indices (the counter alone would wrap at idx = 2^40 and alias idx - 2^40).
+inline uint64_t ct_nonce(Purpose purpose, int noise, uint64_t idx) {
+    return (2 * (uint64_t)purpose + (uint64_t)noise) | ((idx >> 40) << 8);
+}
+inline uint64_t ct_counter(uint64_t idx) { return (idx & ((1ull << 40) - 1)) * kCtStride; }
+// Encryption index space of the client key: explicit raw indices live below kAutoIndexBase; the
+// indices tae_encrypt (and raw calls with TAE_INDEX_AUTO) reserve from next_index live above it,
+// so the two can never collide.
+constexpr uint64_t kAutoIndexBase = 1ull << 63;
 
 inline uint64_t encode_bit(uint64_t bit) { return bit << 63; }
 inline uint64_t decode_bit(uint64_t x) { return ((x + (1ull << 62)) & (1ull << 63)) >> 63; }

@@ -29,8 +29,12 @@ void hip_check(hipError_t e, const char *what);
 struct StageTimes {
     float keyswitch = 0, pbs = 0, pfks = 0, ggsw_fft = 0, vertical_packing = 0, extract = 0, linear = 0;
     int pbs_launches = 0;  // CBS-level PBS launches (one homomorphic_shift_boolean batch each)
+    // the throughput blind-rotation kernel alone (br512x4 launches inside the PBS stage, without the
+    // br512lat remainder) and the ciphertexts those launches processed
+    float pbs_main = 0;
+    double pbs_main_cts = 0;
 };
-enum Stage { ST_KS = 0, ST_PBS, ST_PFKS, ST_FFT, ST_VP, ST_EXTRACT, ST_LINEAR };
+enum Stage { ST_KS = 0, ST_PBS, ST_PFKS, ST_FFT, ST_VP, ST_EXTRACT, ST_LINEAR, ST_PBS_MAIN };
 
 class Engine {
   public:
@@ -95,6 +99,10 @@ class Engine {
     void lwe_add(uint64_t *d_a, const uint64_t *d_b, size_t count);  // a += b (count u64)
 
     void synchronize();
+    // Device-resident caller buffers (TAE_MEM_DEVICE) may have been written on any stream of the
+    // caller (torch's current stream, an RCCL stream): wait for all device work before the engine's
+    // non-blocking stream reads them.
+    void order_after_caller();
     const StageTimes &last_times() const { return times_; }
     void set_timing(bool on) { timing_ = on; }
 
@@ -150,26 +158,17 @@ class Engine {
     void collect_times();
     // int8 MFMA keyswitches (ksgemm.hpp): key limb matrices + digit scratch
     bool mfma_ks_ = false;
-    bool pf_il_ = false;      // PFKS operands row-pair interleaved (ksgemm::op_off), for gemm_g6
-    int glds_gemm_ = 8;       // PFKS GEMM: 8 / 6 / 2 gemm_g6 (LDS-DMA; 4 / 3 / 2 M waves), 0 gemm_big3
-    bool gemm3_ = true;     // PFKS digits as 3 x 6-bit limbs (TAE_GEMM_MA4=1: 4 x 5 bits)
-    bool big_gemm_ = true;  // PFKS on the 256 x 256-tile GEMM (TAE_GEMM_SMALL=1: 128 x 128)
     int8_t *d_pf_bt_ = nullptr, *d_ks_bt_ = nullptr, *d_digits_ = nullptr;
     size_t cap_digits_ = 0;
     int kp_pf_ = 0, kp_ks_ = 0;
     void prepare_mfma_keys();
-    double w16_[10] = {};     // W_16^{1,2,3,6,9} from the FFT table (batched N=512 kernels)
-    bool batched512_ = false; // N == 512, k == 4: multi-ciphertext blind-rotation kernels
     // batched N=1024, k=2 blind rotation (br1024.hpp) for this set's (levels, base_log), or nullptr
     void (*br1024_pbs_)(const uint64_t *, int, const uint64_t *, int, const cplx *, int, uint64_t *, long, uint64_t,
                         uint64_t, const cplx *, const cplx *, const cplx *) = nullptr;
     decltype(br1024_pbs_) br1024_vp_ = nullptr;
-    bool x4_512_ = false;     // ... as 1024-thread workgroups (br512x4.hpp; TAE_BR_X2=1 -> br512x2.hpp)
-    bool lat512_ = false;     // small batches on br512lat.hpp (B <= lat_max_)
-    long lat_max_ = 256;
+    bool x4_512_ = false;     // N = 512, k = 4 (lvl_64): batched blind rotations br512x4 / br512lat
+    long lat_max_ = 256;      // batch size up to which br512lat runs (TAE_BR_LAT_MAX)
     int num_cu_ = 256;
-    bool x5_512_ = false;     // ... with ACC in registers, double-buffered spectra (br512x5.hpp; opt-in TAE_BR_X5=1)
-    bool wide512_ = false;    // ... as 512-thread workgroups (br512x2.hpp; TAE_BR_256=1 -> br512.hpp)
     bool timing_ = false;
     StageTimes times_;
 };

@@ -18,9 +18,7 @@
 
 #include "aes.hpp"
 #include "br512.hpp"
-#include "br512x2.hpp"
 #include "br512x4.hpp"
-#include "br512x5.hpp"
 #include "br512lat.hpp"
 #include "br1024.hpp"
 #include "ksgemm.hpp"
@@ -527,16 +525,6 @@ unsigned grid_for(size_t total) { return (unsigned)std::min<size_t>((total + kTh
 
 constexpr int kBrC = 3;  // ciphertexts per workgroup in the batched N=512 blind rotation
 
-br512::W16 make_w16(const double *w) {
-    br512::W16 W;
-    W.w1 = {w[0], w[1]};
-    W.w2 = {w[2], w[3]};
-    W.w3 = {w[4], w[5]};
-    W.w6 = {w[6], w[7]};
-    W.w9 = {w[8], w[9]};
-    return W;
-}
-
 template <int N>
 size_t br_lds_bytes(int k, int levels) {
     (void)levels;  // ext_product_step works one level at a time
@@ -624,51 +612,23 @@ void Engine::init_common() {
             for (; q < 8; q++) mix_idx_[o][q] = -1;
         }
     }
-    // batched N=512 blind rotation (br512.hpp); TAE_BR_V1=1 forces the one-ciphertext kernels
-    const char *v1 = getenv("TAE_BR_V1");
-    batched512_ = p_.N == 512 && p_.k == 4 && !(v1 && v1[0] == '1');
-    const int w16e[5] = {1, 2, 3, 6, 9};
-    for (int i = 0; i < 5; i++) {
-        w16_[2 * i] = t.w[2 * (w16e[i] * t.M / 16)];
-        w16_[2 * i + 1] = t.w[2 * (w16e[i] * t.M / 16) + 1];
-    }
-    const char *b256 = getenv("TAE_BR_256");
-    wide512_ = batched512_ && !(b256 && b256[0] == '1');
-    // 1024-thread kernel (br512x4.hpp) by default; TAE_BR_X2=1 keeps the 512-thread one
-    const char *bx2 = getenv("TAE_BR_X2");
-    x4_512_ = wide512_ && !(bx2 && bx2[0] == '1') && p_.pbs_b == 12 && p_.cbs_b == 13;
-    // register-ACC / double-buffered variant (br512x5.hpp), opt-in with TAE_BR_X5=1: it needs more
-    // than the 128 VGPRs of 4 waves per SIMD and spills (295 ms vs 205 ms per PBS launch)
-    const char *bx5 = getenv("TAE_BR_X5");
-    x5_512_ = x4_512_ && bx5 && bx5[0] == '1';
-    // small batches: one ciphertext per workgroup, levels in parallel (br512lat.hpp); TAE_BR_LAT_MAX
-    // overrides the batch-size threshold (0 disables)
+    // batched N=512, k=4 blind rotation (params_sqrd_lvl_64): br512x4 for large batches, br512lat for
+    // small ones.  TAE_BR_LAT_MAX (a tuning knob, both sides pinned by tests) is the batch size up
+    // to which br512lat runs (0: never).
+    x4_512_ = p_.N == 512 && p_.k == 4 && p_.pbs_l == 3 && p_.pbs_b == 12 && p_.cbs_l == 1 && p_.cbs_b == 13;
     const char *blat = getenv("TAE_BR_LAT_MAX");
-    lat512_ = x4_512_;
     lat_max_ = blat ? atol(blat) : 256;
     HIPC(hipDeviceGetAttribute(&num_cu_, hipDeviceAttributeMultiprocessorCount, device_));
-    if (batched512_) {
+    if (x4_512_) {
         HIPC(hipFuncSetAttribute((const void *)br512lat::br_kernel<3, 12>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)br512lat::lds_bytes(3)));
-        HIPC(hipFuncSetAttribute((const void *)br512x5::br_kernel<3, true, 12>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        HIPC(hipFuncSetAttribute((const void *)br512x5::br_kernel<1, false, 13>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         HIPC(hipFuncSetAttribute((const void *)br512x4::br_kernel<3, true, 12>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         HIPC(hipFuncSetAttribute((const void *)br512x4::br_kernel<1, false, 13>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        HIPC(hipFuncSetAttribute((const void *)br512x2::br_kernel<3, true, 12>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        HIPC(hipFuncSetAttribute((const void *)br512x2::br_kernel<1, false, 13>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        HIPC(hipFuncSetAttribute((const void *)br512::br_kernel<kBrC, 3, true>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        HIPC(hipFuncSetAttribute((const void *)br512::br_kernel<kBrC, 1, false>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     }
-    // batched N=1024, k=2 blind rotation (br1024.hpp); TAE_BR_V1=1 forces the one-ciphertext kernels
-    if (p_.N == 1024 && p_.k == 2 && !(v1 && v1[0] == '1')) {
+    // batched N=1024, k=2 blind rotation (br1024.hpp); other shapes run the generic kernels
+    if (p_.N == 1024 && p_.k == 2) {
         br1024_pbs_ = br1024::pick(true, p_.pbs_l, p_.pbs_b);
         br1024_vp_ = br1024::pick(false, p_.cbs_l, p_.cbs_b);
         for (auto kf : {br1024_pbs_, br1024_vp_})
@@ -721,25 +681,11 @@ Engine::Engine(const ServerKeyRaw &keys, int device) : p_(keys.p), device_(devic
 
 // Key limb matrices for the int8-MFMA keyswitches (ksgemm.hpp), built once on device.
 void Engine::prepare_mfma_keys() {
-    const char *bg = getenv("TAE_GEMM_SMALL");
-    big_gemm_ = !(bg && bg[0] == '1');
-    const char *g4 = getenv("TAE_GEMM_MA4");
-    gemm3_ = !(g4 && g4[0] == '1');
-    HIPC(hipFuncSetAttribute((const void *)ksgemm::gemm_big<4, 5>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)ksgemm::gemm_big_lds()));
-    HIPC(hipFuncSetAttribute((const void *)ksgemm::gemm_big3<6>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)ksgemm::gemm_big3_lds()));
-    HIPC(hipFuncSetAttribute((const void *)ksgemm::gemm_g6<6, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)ksgemm::gemm_g6_lds<2>()));
-    HIPC(hipFuncSetAttribute((const void *)ksgemm::gemm_g6<6, 3>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)ksgemm::gemm_g6_lds<3>()));
     HIPC(hipFuncSetAttribute((const void *)ksgemm::gemm_g6<6, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)ksgemm::gemm_g6_lds<4>()));
-    // TAE_GEMM_GLDS=0: register-staged gemm_big3; 2 / 6 / 8 (default): gemm_g6 with 2 / 3 / 4 M waves
-    const char *gl = getenv("TAE_GEMM_GLDS");
-    glds_gemm_ = !gl ? 8 : gl[0] == '0' ? 0 : gl[0] == '2' ? 2 : gl[0] == '6' ? 6 : 8;
-    const char *v = getenv("TAE_KS_VALU");
-    mfma_ks_ = !(v && v[0] == '1') && p_.pfks_b * 1 <= 16 && p_.ks_b <= 7;
+    // int8-MFMA keyswitches when the digits fit their limbs (PFKS 17-bit digits as 3 x 6-bit limbs,
+    // KS digits as one byte); otherwise (params_sqrd_lvl_1: pfks base 2^24) the u64 VALU kernels
+    mfma_ks_ = p_.pfks_b <= 16 && p_.ks_b <= 7;
     if (!mfma_ks_) return;
     const int glwe = (int)p_.glwe_len();
     const int kd_pf = (p_.K() + 1) * p_.pfks_l, kd_ks = p_.K() * p_.ks_l;
@@ -749,10 +695,9 @@ void Engine::prepare_mfma_keys() {
     d_pf_bt_ = static_cast<int8_t *>(alloc((size_t)nc_pf * 8 * kp_pf_));
     d_ks_bt_ = static_cast<int8_t *>(alloc((size_t)nc_ks * 8 * kp_ks_));
     dim3 gpf((kp_pf_ + 63) / 64, (nc_pf + 63) / 64), gks((kp_ks_ + 63) / 64, (nc_ks + 63) / 64);
-    // the LDS-DMA GEMMs read both operands row-pair interleaved (ksgemm::op_off)
-    pf_il_ = big_gemm_ && gemm3_ && glds_gemm_ != 0 && kp_pf_ % ksgemm::G4K == 0;
+    // the LDS-DMA GEMM reads both operands row-pair interleaved (ksgemm::op_off; Kp % 128 == 0)
     ksgemm::prep_key<<<gpf, kThreads, 0, stream_>>>(d_pfpksk_, d_pf_bt_, kd_pf, kp_pf_, nc_pf, glwe, glwe,
-                                                    (long)(p_.K() + 1) * p_.pfks_l * glwe, pf_il_);
+                                                    (long)(p_.K() + 1) * p_.pfks_l * glwe, true);
     ksgemm::prep_key<<<gks, kThreads, 0, stream_>>>(d_ksk_, d_ks_bt_, kd_ks, kp_ks_, nc_ks, nc_ks, nc_ks, 0);
     HIPC(hipGetLastError());
     HIPC(hipStreamSynchronize(stream_));
@@ -778,6 +723,7 @@ Engine::Engine(const Params &p, int device, const uint64_t *d_ksk, const uint64_
     : p_(p), device_(device) {
     init_common();
     owns_keys_ = false;
+    order_after_caller();  // the key buffers may still be in flight on the caller's stream (RCCL broadcast)
     d_ksk_ = const_cast<uint64_t *>(d_ksk);
     d_pfpksk_ = const_cast<uint64_t *>(d_pfpksk);
     bsk_to_fourier(d_bsk);
@@ -802,6 +748,11 @@ Engine::~Engine() {
 }
 
 void Engine::synchronize() { HIPC(hipStreamSynchronize(stream_)); }
+
+void Engine::order_after_caller() {
+    HIPC(hipSetDevice(device_));
+    HIPC(hipDeviceSynchronize());
+}
 
 void Engine::reserve(size_t bits, size_t outputs) {
     grow(d_small_, cap_small_, bits * p_.small_len());
@@ -834,48 +785,31 @@ void Engine::keyswitch(const uint64_t *d_in, uint64_t *d_out, size_t B) {
 void Engine::bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint64_t *d_big, size_t B,
                        uint64_t body_add, uint64_t out_add) {
     if (!B) return;
-    if (batched512_ && p_.pbs_l == 3) {
-        const br512::W16 W = make_w16(w16_);
-        const size_t wgs = (B + kBrC - 1) / kBrC;
-        if (lat512_ && (long)B <= lat_max_) {
+    if (x4_512_) {
+        if ((long)B <= lat_max_) {
             br512lat::br_kernel<3, 12><<<(unsigned)B, br512lat::THREADS, br512lat::lds_bytes(3), stream_>>>(
                 d_small, p_.n, d_lut_glwe, d_bsk_f_, d_big, (long)B, body_add, out_add, d_twist_, d_w_);
             HIPC(hipGetLastError());
             return;
         }
-        if (x5_512_) {
-            br512x5::br_kernel<3, true, 12><<<(unsigned)wgs, br512x5::THREADS, br512x5::lds_bytes(), stream_>>>(
-                d_small, p_.n, d_lut_glwe, 0, d_bsk_f_, 0, d_big, (long)B, body_add, out_add, d_twist_, d_w_);
-            HIPC(hipGetLastError());
-            return;
-        }
-        if (x4_512_) {
-            // whole rounds of three ciphertexts per CU on br512x4; a remainder that would leave most
-            // CUs idle in a last round goes to br512lat (one ciphertext per CU, ~0.6x the round time)
-            long bx = (long)B;
-            const long per_round = 3L * num_cu_, rest = (long)B % per_round;
-            if (lat512_ && (long)B > per_round && rest > 0 && rest <= std::min<long>(lat_max_, num_cu_)) bx -= rest;
+        // whole rounds of three ciphertexts per CU on br512x4; a remainder that would leave most
+        // CUs idle in a last round goes to br512lat (one ciphertext per CU, ~0.6x the round time)
+        long bx = (long)B;
+        const long per_round = 3L * num_cu_, rest = (long)B % per_round;
+        if ((long)B > per_round && rest > 0 && rest <= std::min<long>(lat_max_, num_cu_)) bx -= rest;
+        timed(ST_PBS_MAIN, [&] {
             br512x4::br_kernel<3, true, 12><<<(unsigned)((bx + 2) / 3), br512x4::THREADS, br512x4::lds_bytes(),
                                                stream_>>>(d_small, p_.n, d_lut_glwe, 0, d_bsk_f_, 0, d_big, bx,
                                                           body_add, out_add, d_twist_, d_w_);
             HIPC(hipGetLastError());
-            if (bx < (long)B) {
-                br512lat::br_kernel<3, 12><<<(unsigned)(B - bx), br512lat::THREADS, br512lat::lds_bytes(3), stream_>>>(
-                    d_small + (size_t)bx * (p_.n + 1), p_.n, d_lut_glwe, d_bsk_f_, d_big + (size_t)bx * p_.big_len(),
-                    (long)B - bx, body_add, out_add, d_twist_, d_w_);
-                HIPC(hipGetLastError());
-            }
-            return;
-        }
-        if (wide512_) {
-            br512x2::br_kernel<3, true, 12><<<(unsigned)wgs, br512x2::THREADS, br512x2::lds_bytes(), stream_>>>(
-                d_small, p_.n, d_lut_glwe, 0, d_bsk_f_, 0, d_big, (long)B, p_.pbs_b, body_add, out_add, d_twist_, d_w_, W);
+        });
+        if (timing_) times_.pbs_main_cts += (double)bx;
+        if (bx < (long)B) {
+            br512lat::br_kernel<3, 12><<<(unsigned)(B - bx), br512lat::THREADS, br512lat::lds_bytes(3), stream_>>>(
+                d_small + (size_t)bx * (p_.n + 1), p_.n, d_lut_glwe, d_bsk_f_, d_big + (size_t)bx * p_.big_len(),
+                (long)B - bx, body_add, out_add, d_twist_, d_w_);
             HIPC(hipGetLastError());
-            return;
         }
-        br512::br_kernel<kBrC, 3, true><<<(unsigned)wgs, kThreads, br512::lds_bytes(kBrC), stream_>>>(
-            d_small, p_.n, d_lut_glwe, 0, d_bsk_f_, 0, d_big, (long)B, p_.pbs_b, body_add, out_add, d_twist_, d_w_, W);
-        HIPC(hipGetLastError());
         return;
     }
     if (br1024_pbs_) {
@@ -908,59 +842,20 @@ void Engine::pbs_shift_boolean(const uint64_t *d_small, uint64_t *d_big, size_t 
 void Engine::pfks_into_ggsw(const uint64_t *d_big, uint64_t *d_ggsw, size_t B, int level) {
     if (!B) return;
     const int glwe = (int)p_.glwe_len();
-    if (mfma_ks_ && big_gemm_ && gemm3_) {
-        // digits as 3 balanced 6-bit limbs, limb index in the MFMA row tile (ksgemm.hpp gemm_big3)
+    if (mfma_ks_) {
+        // digits as 3 balanced 6-bit limbs, limb index in the MFMA row tile (ksgemm.hpp gemm_g6)
         const int K = p_.K(), kd = (K + 1) * p_.pfks_l;
-        // 192-, 288- and 384-row tiles (64, 96, 128 ciphertexts)
-        const long mtiles = (long)((B + 63) / 64), mt3 = (long)((B + 95) / 96), mt4 = (long)((B + 127) / 128);
-        const size_t rows = std::max({(size_t)mtiles * ksgemm::B3M, (size_t)mt3 * 288, (size_t)mt4 * 384});
-        ensure_digits(d_digits_, cap_digits_, rows, kd, kp_pf_, stream_, pf_il_);
+        const long mt4 = (long)((B + 127) / 128);  // 384-row tiles (128 ciphertexts x 3 limbs)
+        ensure_digits(d_digits_, cap_digits_, (size_t)mt4 * 384, kd, kp_pf_, stream_, true);
         const size_t thr = B * (size_t)(K + 1);
         ksgemm::prep_digits3<6><<<(unsigned)((thr + 255) / 256), 256, 0, stream_>>>(
-            d_big, K + 1, d_digits_, (long)B, K + 1, kp_pf_, p_.pfks_b, p_.pfks_l, pf_il_);
+            d_big, K + 1, d_digits_, (long)B, K + 1, kp_pf_, p_.pfks_b, p_.pfks_l, true);
         const int ncols = (p_.k + 1) * glwe;
         const long out_stride = (long)p_.cbs_l * ncols;
         const long ntiles = ((long)ncols * 8 + ksgemm::BTN - 1) / ksgemm::BTN;
         uint64_t *dst = d_ggsw + (size_t)(level - 1) * ncols;
-        if (pf_il_ && glds_gemm_ == 8) {
-            ksgemm::gemm_g6<6, 4><<<(unsigned)(mt4 * ntiles), 1024, ksgemm::gemm_g6_lds<4>(), stream_>>>(
-                d_digits_, d_pf_bt_, kp_pf_, mt4, ncols, dst, out_stride, (long)B);
-        } else if (pf_il_ && glds_gemm_ == 6) {
-            ksgemm::gemm_g6<6, 3><<<(unsigned)(mt3 * ntiles), 768, ksgemm::gemm_g6_lds<3>(), stream_>>>(
-                d_digits_, d_pf_bt_, kp_pf_, mt3, ncols, dst, out_stride, (long)B);
-        } else if (pf_il_) {
-            ksgemm::gemm_g6<6, 2><<<(unsigned)(mtiles * ntiles), 512, ksgemm::gemm_g6_lds<2>(), stream_>>>(
-                d_digits_, d_pf_bt_, kp_pf_, mtiles, ncols, dst, out_stride, (long)B);
-        } else {
-            ksgemm::gemm_big3<6><<<(unsigned)(mtiles * ntiles), 512, ksgemm::gemm_big3_lds(), stream_>>>(
-                d_digits_, d_pf_bt_, kp_pf_, mtiles, ncols, dst, out_stride, (long)B);
-        }
-        HIPC(hipGetLastError());
-        return;
-    }
-    if (mfma_ks_) {
-        constexpr int MA = 4, LB = 5;  // 17-bit signed digits as 4 balanced 5-bit limbs
-        const int K = p_.K(), kd = (K + 1) * p_.pfks_l;
-        ensure_digits(d_digits_, cap_digits_, B * MA, kd, kp_pf_, stream_);
-        const size_t thr = B * (size_t)(K + 1);
-        ksgemm::prep_digits<MA, LB><<<(unsigned)((thr + 255) / 256), 256, 0, stream_>>>(
-            d_big, K + 1, d_digits_, (long)B, K + 1, kp_pf_, p_.pfks_b, p_.pfks_l);
-        const int ncols = (p_.k + 1) * glwe;
-        const long out_stride = (long)p_.cbs_l * ncols;
-        if (big_gemm_) {
-            const long mtiles = (long)((B * MA + ksgemm::BTM - 1) / ksgemm::BTM);
-            const long ntiles = ((long)ncols * 8 + ksgemm::BTN - 1) / ksgemm::BTN;
-            ksgemm::gemm_big<MA, LB><<<(unsigned)(mtiles * ntiles), 512, ksgemm::gemm_big_lds(), stream_>>>(
-                d_digits_, d_pf_bt_, kp_pf_, (long)B * MA, mtiles, ncols, d_ggsw + (size_t)(level - 1) * ncols,
-                out_stride, (long)B, nullptr, 0, -1);
-            HIPC(hipGetLastError());
-            return;
-        }
-        const long mtiles = (long)((B * MA + ksgemm::TM - 1) / ksgemm::TM);
-        const long ntiles = ((long)ncols * 8 + ksgemm::TN - 1) / ksgemm::TN;
-        ksgemm::gemm<MA, LB><<<(unsigned)(mtiles * ntiles), 256, 0, stream_>>>(
-            d_digits_, d_pf_bt_, kp_pf_, (long)B * MA, mtiles, ncols, d_ggsw + (size_t)(level - 1) * ncols, out_stride,
-            (long)B, nullptr, 0, -1);
+        ksgemm::gemm_g6<6, 4><<<(unsigned)(mt4 * ntiles), 1024, ksgemm::gemm_g6_lds<4>(), stream_>>>(
+            d_digits_, d_pf_bt_, kp_pf_, mt4, ncols, dst, out_stride, (long)B);
         HIPC(hipGetLastError());
         return;
     }
@@ -1037,29 +932,10 @@ void Engine::vertical_packing(const cplx *d_ggsw_f, size_t G, int n_in, const ui
         vertical_packing_tree(d_ggsw_f, G, n_in, n_in - logN, d_lut, n_out, d_out);
         return;
     }
-    if (batched512_ && p_.cbs_l == 1) {
-        const br512::W16 W = make_w16(w16_);
+    if (x4_512_) {
         const size_t wgs = G * (size_t)((n_out + kBrC - 1) / kBrC);
-        if (x5_512_) {
-            br512x5::br_kernel<1, false, 13><<<(unsigned)wgs, br512x5::THREADS, br512x5::lds_bytes(), stream_>>>(
-                nullptr, 0, d_lut, n_out, d_ggsw_f, n_in, d_out, (long)G, 0, 0, d_twist_, d_w_);
-            HIPC(hipGetLastError());
-            return;
-        }
-        if (x4_512_) {
-            br512x4::br_kernel<1, false, 13><<<(unsigned)wgs, br512x4::THREADS, br512x4::lds_bytes(), stream_>>>(
-                nullptr, 0, d_lut, n_out, d_ggsw_f, n_in, d_out, (long)G, 0, 0, d_twist_, d_w_);
-            HIPC(hipGetLastError());
-            return;
-        }
-        if (wide512_) {
-            br512x2::br_kernel<1, false, 13><<<(unsigned)wgs, br512x2::THREADS, br512x2::lds_bytes(), stream_>>>(
-                nullptr, 0, d_lut, n_out, d_ggsw_f, n_in, d_out, (long)G, p_.cbs_b, 0, 0, d_twist_, d_w_, W);
-            HIPC(hipGetLastError());
-            return;
-        }
-        br512::br_kernel<kBrC, 1, false><<<(unsigned)wgs, kThreads, br512::lds_bytes(kBrC), stream_>>>(
-            nullptr, 0, d_lut, n_out, d_ggsw_f, n_in, d_out, (long)G, p_.cbs_b, 0, 0, d_twist_, d_w_, W);
+        br512x4::br_kernel<1, false, 13><<<(unsigned)wgs, br512x4::THREADS, br512x4::lds_bytes(), stream_>>>(
+            nullptr, 0, d_lut, n_out, d_ggsw_f, n_in, d_out, (long)G, 0, 0, d_twist_, d_w_);
         HIPC(hipGetLastError());
         return;
     }
@@ -1115,7 +991,7 @@ void Engine::collect_times() {
         float ms = 0;
         HIPC(hipEventElapsedTime(&ms, sp.a, sp.b));
         float *dst[] = {&times_.keyswitch, &times_.pbs, &times_.pfks, &times_.ggsw_fft, &times_.vertical_packing,
-                        &times_.extract, &times_.linear};
+                        &times_.extract, &times_.linear, &times_.pbs_main};
         *dst[sp.stage] += ms;
     }
     spans_.clear();

@@ -241,123 +241,7 @@ __global__ void __launch_bounds__(256, 2)
         }
 }
 
-// ---- the big-tile GEMM (PFKS): 256 x 256 workgroup tile, 512 threads = 8 waves (2 along M x 4
-// along N), each wave 128 x 64 = 4 x 2 MFMA tiles.  A 128 x 128 tile pair streams 32 KB per 2048
-// MFMA-cycles of a CU, which outran the L2 (~35 TB/s); the 256 x 256 tile halves the bytes per
-// MFMA.  One workgroup per CU (147 KB LDS, double-buffered 144-B rows).  Same epilogue as gemm. ----
-constexpr int BTM = 256, BTN = 256;
-
-template <int MA, int LB>
-__global__ void __launch_bounds__(512, 1)
-    gemm_big(const int8_t *__restrict__ A, const int8_t *__restrict__ Bt, int Kp, long Mrows, long mtiles, int ncols,
-             uint64_t *__restrict__ out, long out_stride, long B, const uint64_t *__restrict__ body_in,
-             long body_stride, int body_col) {
-    extern __shared__ __align__(16) int8_t smem_g[];
-    auto sA = [&](int b) { return smem_g + b * BTM * LROW; };
-    auto sB = [&](int b) { return smem_g + 2 * BTM * LROW + b * BTN * LROW; };
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int wm = wave >> 2, wn = wave & 3;
-    constexpr long GN = 16;
-    const long ntiles = (((long)ncols * 8) + BTN - 1) / BTN;
-    const long gsz = GN * mtiles;
-    const long ng = blockIdx.x / gsz, rr = blockIdx.x - ng * gsz;
-    const long gw = min(GN, ntiles - ng * GN);
-    const long mt = rr / gw, nt = ng * GN + (rr - (rr / gw) * gw);
-    const long row0 = mt * BTM;
-    const long col8_0 = nt * BTN;
-    const long N8 = (long)ncols * 8;
-
-    // loader: chunk c = tid + 512 t (t < 4): row = c >> 3 (0..255), 16-byte column kc = c & 7
-    v4i ra[4], rb[4];
-    auto gload = [&](int k0) {
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-            const int c = tid + 512 * t, r = c >> 3, kc = c & 7;
-            const long ar = row0 + r, br = col8_0 + r;
-            ra[t] = ar < Mrows ? *reinterpret_cast<const v4i *>(A + ar * Kp + k0 + kc * 16) : v4i{0, 0, 0, 0};
-            rb[t] = br < N8 ? *reinterpret_cast<const v4i *>(Bt + br * Kp + k0 + kc * 16) : v4i{0, 0, 0, 0};
-        }
-    };
-    auto lstore = [&](int buf) {
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-            const int c = tid + 512 * t, r = c >> 3, kc = c & 7;
-            *reinterpret_cast<v4i *>(&sA(buf)[r * LROW + kc * 16]) = ra[t];
-            *reinterpret_cast<v4i *>(&sB(buf)[r * LROW + kc * 16]) = rb[t];
-        }
-    };
-
-    v16i acc[4][2];
-#pragma unroll
-    for (int a = 0; a < 4; a++)
-#pragma unroll
-        for (int b = 0; b < 2; b++) acc[a][b] = v16i{0};
-
-    const int r = lane & 31, h = lane >> 5;
-    gload(0);
-    lstore(0);
-    __syncthreads();
-    const int nk = Kp / TK;
-    for (int ks = 0; ks < nk; ks++) {
-        const int cur = ks & 1;
-        if (ks + 1 < nk) gload((ks + 1) * TK);
-#pragma unroll
-        for (int kk = 0; kk < TK / 32; kk++) {
-            // the next tile's LDS stores go out between this tile's MFMAs (buffer cur ^ 1 was last
-            // read before the previous barrier)
-            if (kk == TK / 64 && ks + 1 < nk) lstore(cur ^ 1);
-            v4i fa[4], fb[2];
-#pragma unroll
-            for (int ti = 0; ti < 4; ti++)
-                fa[ti] = *reinterpret_cast<const v4i *>(&sA(cur)[(wm * 128 + ti * 32 + r) * LROW + kk * 32 + h * 16]);
-#pragma unroll
-            for (int tj = 0; tj < 2; tj++)
-                fb[tj] = *reinterpret_cast<const v4i *>(&sB(cur)[(wn * 64 + tj * 32 + r) * LROW + kk * 32 + h * 16]);
-#pragma unroll
-            for (int ti = 0; ti < 4; ti++)
-#pragma unroll
-                for (int tj = 0; tj < 2; tj++)
-                    acc[ti][tj] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[ti], fb[tj], acc[ti][tj], 0, 0, 0);
-        }
-        if (ks + 1 < nk) __syncthreads();
-    }
-
-    const int j = r & 7;
-#pragma unroll
-    for (int ti = 0; ti < 4; ti++)
-#pragma unroll
-        for (int tj = 0; tj < 2; tj++) {
-            const long col = (col8_0 + wn * 64 + tj * 32 + r) >> 3;
-#pragma unroll
-            for (int g = 0; g < 16 / MA; g++) {
-                uint64_t v = 0;
-#pragma unroll
-                for (int m = 0; m < MA; m++) {
-                    const int q = g * MA + m;
-                    const int sh = LB * m + 8 * j;
-                    const uint64_t p = (uint64_t)(int64_t)acc[ti][tj][q];
-                    v += sh < 64 ? (p << sh) : 0;
-                }
-#pragma unroll
-                for (int x = 1; x < 8; x <<= 1) {
-                    const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-                    const uint32_t olo = __shfl_xor((int)lo, x, 64), ohi = __shfl_xor((int)hi, x, 64);
-                    v += ((uint64_t)ohi << 32) | olo;
-                }
-                const int q0 = g * MA;
-                const int row = (q0 & 3) + 8 * (q0 >> 2) + 4 * h;
-                const long grow = row0 + wm * 128 + ti * 32 + row;
-                const long b = grow / MA;
-                if (j == 0 && col < ncols && b < B) {
-                    uint64_t o = 0 - v;
-                    if (col == body_col) o += body_in[b * body_stride];
-                    out[b * out_stride + col] = o;
-                }
-            }
-        }
-}
-
-inline size_t gemm_big_lds() { return (size_t)2 * (BTM + BTN) * LROW; }
+constexpr int BTN = 256;  // key columns (col, limb) per PFKS workgroup tile
 
 // ---- PFKS with 3 balanced 6-bit digit limbs (|d| <= 2^16 fits [-133152, 128991]; every i32 partial
 // sum stays exact: 32 * 128 * 4224 < 2^31), 25% fewer MFMAs than 4 x 5 bits.  The limb index sits in
@@ -401,125 +285,7 @@ __global__ void __launch_bounds__(256) prep_digits3(const uint64_t *__restrict__
     }
 }
 
-constexpr int B3M = 192;  // rows per workgroup tile: 2 waves x (3 limbs x 32 ciphertexts)
-
-template <int LB3>
-__global__ void __launch_bounds__(512, 1)
-    gemm_big3(const int8_t *__restrict__ A, const int8_t *__restrict__ Bt, int Kp, long mtiles, int ncols,
-              uint64_t *__restrict__ out, long out_stride, long B) {
-    extern __shared__ __align__(16) int8_t smem_g[];
-    auto sA = [&](int b) { return smem_g + b * B3M * LROW; };
-    auto sB = [&](int b) { return smem_g + 2 * B3M * LROW + b * BTN * LROW; };
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int wm = wave >> 2, wn = wave & 3;
-    constexpr long GN = 16;
-    const long ntiles = (((long)ncols * 8) + BTN - 1) / BTN;
-    const long gsz = GN * mtiles;
-    const long ng = blockIdx.x / gsz, rr = blockIdx.x - ng * gsz;
-    const long gw = min(GN, ntiles - ng * GN);
-    const long mt = rr / gw, nt = ng * GN + (rr - (rr / gw) * gw);
-    const long row0 = mt * B3M;
-    const long col8_0 = nt * BTN;
-    const long N8 = (long)ncols * 8;
-    const long Mrows = mtiles * B3M;  // the digit buffer is padded to whole tiles
-
-    // loader: A 192 rows x 8 chunks (3 per thread), B 256 rows x 8 chunks (4 per thread)
-    v4i ra[3], rb[4];
-    auto gload = [&](int k0) {
-#pragma unroll
-        for (int t = 0; t < 3; t++) {
-            const int c = tid + 512 * t, r = c >> 3, kc = c & 7;
-            ra[t] = *reinterpret_cast<const v4i *>(A + (row0 + r) * Kp + k0 + kc * 16);
-        }
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-            const int c = tid + 512 * t, r = c >> 3, kc = c & 7;
-            const long br = col8_0 + r;
-            rb[t] = br < N8 ? *reinterpret_cast<const v4i *>(Bt + br * Kp + k0 + kc * 16) : v4i{0, 0, 0, 0};
-        }
-    };
-    auto lstore = [&](int buf) {
-#pragma unroll
-        for (int t = 0; t < 3; t++) {
-            const int c = tid + 512 * t, r = c >> 3, kc = c & 7;
-            *reinterpret_cast<v4i *>(&sA(buf)[r * LROW + kc * 16]) = ra[t];
-        }
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-            const int c = tid + 512 * t, r = c >> 3, kc = c & 7;
-            *reinterpret_cast<v4i *>(&sB(buf)[r * LROW + kc * 16]) = rb[t];
-        }
-    };
-    (void)Mrows;
-
-    v16i acc[3][2];
-#pragma unroll
-    for (int a = 0; a < 3; a++)
-#pragma unroll
-        for (int b = 0; b < 2; b++) acc[a][b] = v16i{0};
-
-    const int r = lane & 31, h = lane >> 5;
-    gload(0);
-    lstore(0);
-    __syncthreads();
-    const int nk = Kp / TK;
-    for (int ks = 0; ks < nk; ks++) {
-        const int cur = ks & 1;
-        if (ks + 1 < nk) gload((ks + 1) * TK);
-        // fragments of step kk + 1 are read from LDS while the MFMAs of step kk run
-        v4i fa[2][3], fb[2][2];
-        auto ldfrag = [&](int kk, v4i *xa, v4i *xb) {
-#pragma unroll
-            for (int m = 0; m < 3; m++)
-                xa[m] = *reinterpret_cast<const v4i *>(&sA(cur)[(wm * 96 + m * 32 + r) * LROW + kk * 32 + h * 16]);
-#pragma unroll
-            for (int tj = 0; tj < 2; tj++)
-                xb[tj] = *reinterpret_cast<const v4i *>(&sB(cur)[(wn * 64 + tj * 32 + r) * LROW + kk * 32 + h * 16]);
-        };
-        ldfrag(0, fa[0], fb[0]);
-#pragma unroll
-        for (int kk = 0; kk < TK / 32; kk++) {
-            if (kk == TK / 64 && ks + 1 < nk) lstore(cur ^ 1);
-            if (kk + 1 < TK / 32) ldfrag(kk + 1, fa[(kk + 1) & 1], fb[(kk + 1) & 1]);
-#pragma unroll
-            for (int m = 0; m < 3; m++)
-#pragma unroll
-                for (int tj = 0; tj < 2; tj++)
-                    acc[m][tj] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[kk & 1][m], fb[kk & 1][tj], acc[m][tj], 0, 0, 0);
-        }
-        if (ks + 1 < nk) __syncthreads();
-    }
-
-    const int j = r & 7;
-    const long b0 = (mt * 2 + wm) * 32;
-#pragma unroll
-    for (int tj = 0; tj < 2; tj++) {
-        const long col = (col8_0 + wn * 64 + tj * 32 + r) >> 3;
-#pragma unroll
-        for (int q = 0; q < 16; q++) {
-            uint64_t v = 0;
-#pragma unroll
-            for (int m = 0; m < 3; m++) {
-                const int sh = LB3 * m + 8 * j;
-                const uint64_t p = (uint64_t)(int64_t)acc[m][tj][q];
-                v += sh < 64 ? (p << sh) : 0;  // 6 m + 8 j reaches 68
-
-            }
-#pragma unroll
-            for (int x = 1; x < 8; x <<= 1) {
-                const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-                const uint32_t olo = __shfl_xor((int)lo, x, 64), ohi = __shfl_xor((int)hi, x, 64);
-                v += ((uint64_t)ohi << 32) | olo;
-            }
-            const long b = b0 + (q & 3) + 8 * (q >> 2) + 4 * h;
-            if (j == 0 && col < ncols && b < B) out[b * out_stride + col] = 0 - v;
-        }
-    }
-}
-
-inline size_t gemm_big3_lds() { return (size_t)2 * (B3M + BTN) * LROW; }
-
-// ---- gemm_g6: the gemm_big3 product with LDS-DMA staging (default PFKS GEMM) ----
+// ---- gemm_g6: the PFKS GEMM (3-limb digits, LDS-DMA staging) ----
 // - Staging: global_load_lds (16 B per lane, no VGPR staging, no ds_write) into a ring of G4S stages
 //   of 64-byte K steps; two steps stay in flight across the per-step barrier by a counted vmcnt
 //   (cdna_hip_programming.md section 5: "Async global->LDS copy", "Pipelining across barriers").
@@ -528,11 +294,12 @@ inline size_t gemm_big3_lds() { return (size_t)2 * (B3M + BTN) * LROW; }
 //   on the fragment reads.
 // - Operands row-pair interleaved in HBM (op_off): one K step of two rows is one 128-byte line.
 // - WM x 4 waves of 96 x 64 (3 limbs x 32 ciphertexts by 64 key columns), workgroup tile
-//   96 WM x 256.  WM = 4 (default, 1024 threads, 384 x 256, 160 KiB ring) moves 30% fewer operand
-//   bytes per MFMA than WM = 2 (192 x 256) and runs four MFMA streams per SIMD: 22.5 -> 20.1 ms per
+//   96 WM x 256.  WM = 4 (1024 threads, 384 x 256, 160 KiB ring) moves 30% fewer operand bytes per
+//   MFMA than WM = 2 (192 x 256) and runs four MFMA streams per SIMD: 22.5 -> 20.1 ms per
 //   16384-ciphertext launch (WM = 3: 21.0).  The 6 WM + 16 pieces of 16 rows per stage are dealt
 //   round-robin over the waves.
-// - Same limbs and epilogue as gemm_big3: bit-identical results.
+// - Epilogue: the three limb partial sums of a (ciphertext, key limb j) combine in-lane with shifts,
+//   the 8 key limbs across 8 lanes: bit-identical to the u64 loop.
 #ifndef TAE_G4S
 constexpr int G4K = 64, G4S = 4;                      // K bytes per step, ring stages
 #else

@@ -202,6 +202,7 @@ void Context::run8(const uint64_t *in, size_t in_len, uint64_t *out, size_t out_
     }
     const uint64_t *dl = d_lut ? d_lut->as<uint64_t>() : nullptr;
     if (device_mem) {
+        engine_->order_after_caller();
         fn(in, out, dl);
         engine_->synchronize();
         return;
@@ -247,6 +248,7 @@ void Context::circuit_bootstrap_raw(const uint64_t *bits, size_t groups, int n_i
                              engine_->stream()),
               "lut upload");
     if (device_mem) {
+        engine_->order_after_caller();
         engine_->circuit_bootstrap(bits, groups, n_in, d_lut.as<uint64_t>(), lut.output_bits, out);
         engine_->synchronize();
         return;
@@ -371,6 +373,7 @@ void Context::aes_encrypt_blocks_raw(const uint64_t *rk, const uint64_t *blocks,
         std::lock_guard<std::mutex> g(mu_);
         hip_check(hipSetDevice(engine_->device()), "hipSetDevice");
         if (device_mem) {
+            engine_->order_after_caller();
             engine_->aes8_encrypt_blocks(rk, blocks, n_blocks, rounds, out);
             engine_->synchronize();
             return;
@@ -396,6 +399,7 @@ void Context::aes_encrypt_blocks_raw(const uint64_t *rk, const uint64_t *blocks,
     hip_check(hipSetDevice(engine_->device()), "hipSetDevice");
     const size_t L = params().big_len();
     if (device_mem) {
+        engine_->order_after_caller();
         engine_->aes_encrypt_blocks(rk, blocks, n_blocks, rounds, out);
         engine_->synchronize();
         return;
@@ -564,7 +568,7 @@ void Context::aes_key_schedule_raw(const uint64_t *key, uint64_t *expanded, bool
     const size_t L = bit_len();
     std::vector<uint64_t> hk(128 * L);
     if (device_mem) {
-        hip_check(hipSetDevice(engine_->device()), "hipSetDevice");
+        engine_->order_after_caller();
         hip_check(hipMemcpy(hk.data(), key, hk.size() * 8, hipMemcpyDeviceToHost), "download key");
     } else {
         std::memcpy(hk.data(), key, hk.size() * 8);

@@ -7,7 +7,7 @@ from ._native import (PARAMS_SQRD_LVL_1, PARAMS_SQRD_LVL_4, PARAMS_SQRD_LVL_64, 
                       PARAMS_WOPPBS_8BIT, NoDevice, NoiseNotIndependent, NoiseTooBig, TaeError, bit_len, device_count,
                       get_params, lib)
 from .tfhe import (BitCt, ClientKey, Cleartext, FheContext, WopbsLUT, client_key_from_seed, context_from_raw, decode_bit, encode_bit,
-                   generate_keys, generate_keys_raw, key_file_info, load_keys, save_keys)
+                   generate_keys, generate_keys_raw, key_file_info, load_keys, save_keys, server_key_sizes, generate_multivariate_luts)
 from . import aes_128
 
 __all__ = [
@@ -15,5 +15,5 @@ __all__ = [
     "bit_len", "NoDevice",
     "NoiseNotIndependent", "NoiseTooBig", "TaeError", "device_count", "get_params", "lib", "BitCt", "ClientKey",
     "Cleartext", "FheContext", "WopbsLUT", "client_key_from_seed", "context_from_raw", "decode_bit", "encode_bit", "generate_keys",
-    "generate_keys_raw", "aes_128", "key_file_info", "load_keys", "save_keys",
+    "generate_keys_raw", "aes_128", "key_file_info", "load_keys", "save_keys", "server_key_sizes", "generate_multivariate_luts",
 ]

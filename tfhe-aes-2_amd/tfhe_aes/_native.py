@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("TAE_LIB_PATH") or os.path.join(_HERE, "libtfhe_aes_am
 
 TAE_OK, TAE_E_NOISE, TAE_E_INDEP, TAE_E_PARAM, TAE_E_HIP, TAE_E_ARG, TAE_E_NODEV = range(7)
 TAE_MEM_HOST, TAE_MEM_DEVICE = 0, 1
+TAE_INDEX_AUTO = 2**64 - 1  # tae_encrypt_*_raw: reserve fresh encryption indices from the key's counter
 PARAMS_SQRD_LVL_1, PARAMS_SQRD_LVL_4, PARAMS_SQRD_LVL_64, PARAMS_SQRD_LVL_256 = 0, 1, 2, 3
 PARAMS_WOPPBS_8BIT = 4  # shortint_woppbs_8bit.rs:39-86 (bits under the small key)
 
@@ -31,6 +32,7 @@ EXPORTED = [
     "tae_synchronize", "tae_set_timing", "tae_last_stage_times", "tae_bit_len", "tae_encrypt_ints_raw",
     "tae_decrypt_ints_raw", "tae_bootstrap_from_bits_raw", "tae_extract_bits_raw", "tae_aes_key_schedule_raw",
     "tae_last_stage_times_v2", "tae_keys_save", "tae_keys_file_info", "tae_keys_load",
+    "tae_last_stage_times_v3", "tae_generate_multivariate_luts", "tae_xor_batch",
 ]
 TAE_KEYS_CLIENT, TAE_KEYS_SERVER = 1, 2
 
@@ -120,6 +122,9 @@ def lib() -> C.CDLL:
         "tae_extract_bits_raw": ([vp, vp, sz, vp, C.c_int], C.c_int),
         "tae_aes_key_schedule_raw": ([vp, vp, vp, C.c_int], C.c_int),
         "tae_last_stage_times_v2": ([vp, C.POINTER(C.c_float)], C.c_int),
+        "tae_last_stage_times_v3": ([vp, C.POINTER(C.c_double)], C.c_int),
+        "tae_generate_multivariate_luts": ([C.c_int, C.c_int, C.c_int, vp, vp, sz], C.c_int),
+        "tae_xor_batch": ([vp, vp, vp, sz, vp, vp, vp, C.c_int], C.c_int),
         "tae_keys_save": ([C.c_char_p, C.c_int, vp, vp, vp, vp], C.c_int),
         "tae_keys_file_info": ([C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int)], C.c_int),
         "tae_keys_load": ([C.c_char_p, vpp, vp, vp, vp], C.c_int),

@@ -18,7 +18,8 @@ from . import _native as N
 from ._native import check, lib
 
 __all__ = ["Cleartext", "BitCt", "FheContext", "ClientKey", "WopbsLUT", "encode_bit", "decode_bit",
-           "generate_keys", "generate_keys_raw", "client_key_from_seed", "context_from_raw"]
+           "generate_keys", "generate_keys_raw", "client_key_from_seed", "context_from_raw", "server_key_sizes",
+           "generate_multivariate_luts"]
 
 
 @dataclass(frozen=True)
@@ -198,11 +199,33 @@ class FheContext:
         check(lib().tae_set_timing(self._h, 1 if on else 0))
 
     def last_stage_times(self) -> dict:
-        arr = (C.c_float * 8)()
-        check(lib().tae_last_stage_times_v2(self._h, arr))
+        arr = (C.c_double * 10)()
+        check(lib().tae_last_stage_times_v3(self._h, arr))
         d = dict(zip(("keyswitch", "pbs", "pfks", "ggsw_fft", "vertical_packing", "extract_bits", "linear"), list(arr)))
         d["pbs_launches"] = int(arr[7])
+        d["pbs_main"], d["pbs_main_cts"] = arr[8], arr[9]
         return d
+
+    def xor_batch(self, lhs: np.ndarray, rhs: np.ndarray, lhs_noise_sq=None, rhs_noise_sq=None):
+        """BitXorAssign over whole bit arrays (xor_state, data_model.rs:270-274): lhs += rhs in place
+        (host arrays [count][lwe]); with squared noise levels given, NoiseTooBig is enforced and the
+        summed levels are returned."""
+        if not (isinstance(lhs, np.ndarray) and lhs.dtype == np.uint64 and lhs.flags.c_contiguous):
+            raise ValueError("lhs must be a C-contiguous uint64 array (updated in place)")
+        rhs = np.ascontiguousarray(rhs, dtype=np.uint64)
+        if lhs.size != rhs.size or lhs.size % self.lwe_size:
+            raise ValueError("lhs and rhs must hold the same whole number of bit ciphertexts")
+        count = lhs.size // self.lwe_size
+        ln = rn = out = None
+        if lhs_noise_sq is not None:
+            ln = np.ascontiguousarray(lhs_noise_sq, dtype=np.uint64).ravel()
+            rn = np.ascontiguousarray(rhs_noise_sq, dtype=np.uint64).ravel()
+            if ln.size != count or rn.size != count:
+                raise ValueError("one squared noise level per bit ciphertext")
+            out = np.zeros(count, dtype=np.uint64)
+        p = lambda a: a.ctypes.data_as(C.c_void_p) if a is not None else None
+        check(lib().tae_xor_batch(self._h, p(lhs), p(rhs), count, p(ln), p(rn), p(out), N.TAE_MEM_HOST))
+        return out
 
 
 class ClientKey:
@@ -233,7 +256,10 @@ class ClientKey:
         check(lib().tae_decrypt(self._h, bit._h, C.byref(v)))
         return Cleartext(v.value)
 
-    def encrypt_bits_raw(self, bits, start_index: int) -> np.ndarray:
+    def encrypt_bits_raw(self, bits, start_index: int | None = None) -> np.ndarray:
+        """[count][lwe] ciphertexts of `bits` at encryption indices start_index.. (explicit, below 2^63,
+        never reused for another plaintext) or, with start_index=None, fresh indices from the key."""
+        start_index = N.TAE_INDEX_AUTO if start_index is None else start_index
         bits = np.ascontiguousarray(np.asarray(bits, dtype=np.uint8).ravel())
         out = np.zeros((bits.size, self.lwe_size), dtype=np.uint64)
         check(lib().tae_encrypt_bits_raw(self._h, bits.ctypes.data_as(C.c_void_p), bits.size, start_index,
@@ -248,7 +274,8 @@ class ClientKey:
         return out
 
     # 8-bit model integers: shortint encrypt_without_padding / decrypt_without_padding
-    def encrypt_ints_raw(self, values, start_index: int) -> np.ndarray:
+    def encrypt_ints_raw(self, values, start_index: int | None = None) -> np.ndarray:
+        start_index = N.TAE_INDEX_AUTO if start_index is None else start_index
         values = np.ascontiguousarray(np.asarray(values, dtype=np.uint8).ravel())
         out = np.zeros((values.size, self.int_size), dtype=np.uint64)
         check(lib().tae_encrypt_ints_raw(self._h, values.ctypes.data_as(C.c_void_p), values.size, start_index,
@@ -268,6 +295,18 @@ class ClientKey:
         glwe = np.zeros(p["k"] * p["N"], dtype=np.uint64)
         check(lib().tae_client_key_secrets(self._h, lwe.ctypes.data_as(C.c_void_p), glwe.ctypes.data_as(C.c_void_p)))
         return lwe, glwe
+
+
+def generate_multivariate_luts(poly_size: int, input_bits: int, output_bits: int, f: Callable[[int], int]) -> np.ndarray:
+    """generate_multivariate_luts (shortint_woppbs_1bit.rs:366-403) for any polynomial size, no context:
+    [output_bits * (poly_size << max(0, input_bits - log2 poly_size))] u64 (the reference's exact layout)."""
+    tab = np.array([f(v) & 0xFFFFFFFFFFFFFFFF for v in range(1 << input_bits)], dtype=np.uint64)
+    log_n = poly_size.bit_length() - 1
+    n = output_bits * (poly_size << max(0, input_bits - log_n))
+    out = np.zeros(n, dtype=np.uint64)
+    check(lib().tae_generate_multivariate_luts(poly_size, input_bits, output_bits, tab.ctypes.data_as(C.c_void_p),
+                                               out.ctypes.data_as(C.c_void_p), n))
+    return out
 
 
 def generate_keys(param_set: int = N.PARAMS_SQRD_LVL_64, seed: bytes | None = None, device: int = 0,
@@ -302,9 +341,41 @@ def client_key_from_seed(param_set: int, seed: bytes) -> ClientKey:
     return ClientKey(ck.value, param_set)
 
 
+def server_key_sizes(param_set: int) -> tuple:
+    """u64 lengths of (ksk, bsk, pfpksk) for the parameter set (tae_server_key_sizes)."""
+    sizes = [C.c_size_t() for _ in range(3)]
+    check(lib().tae_server_key_sizes(param_set, *[C.byref(s) for s in sizes]))
+    return tuple(s.value for s in sizes)
+
+
+def _checked_key_arrays(param_set: int, keys) -> list:
+    """The three raw server-key arrays as contiguous uint64 of exactly the sizes the parameter set
+    needs (the C side reads that many words from each pointer)."""
+    keys = list(keys)
+    if len(keys) != 3:
+        raise ValueError("server keys are (ksk, bsk, pfpksk)")
+    out = []
+    for name, k, n in zip(("ksk", "bsk", "pfpksk"), keys, server_key_sizes(param_set)):
+        a = np.asarray(k)
+        if a.dtype not in (np.uint64, np.int64):
+            raise ValueError(f"{name}: expected 64-bit integer words, got {a.dtype}")
+        a = np.ascontiguousarray(a).view(np.uint64).ravel()
+        if a.size != n:
+            raise ValueError(f"{name}: expected {n} u64 words for parameter set {param_set}, got {a.size}")
+        out.append(a)
+    return out
+
+
 def context_from_raw(param_set: int, keys, device: int = 0, mem: int = N.TAE_MEM_HOST) -> FheContext:
-    """Server context from raw keys: numpy arrays (mem=HOST) or device pointers as ints (mem=DEVICE)."""
-    ptrs = [k.ctypes.data_as(C.c_void_p) if isinstance(k, np.ndarray) else C.c_void_p(int(k)) for k in keys]
+    """Server context from raw keys: numpy arrays (mem=HOST) or device pointers as ints (mem=DEVICE;
+    the caller guarantees each buffer holds server_key_sizes(param_set) words and has been written)."""
+    if mem == N.TAE_MEM_HOST:
+        arrs = _checked_key_arrays(param_set, keys)
+        ptrs = [a.ctypes.data_as(C.c_void_p) for a in arrs]
+    else:
+        ptrs = [C.c_void_p(int(k)) for k in keys]
+        if len(ptrs) != 3 or not all(p.value for p in ptrs):
+            raise ValueError("device keys are three non-null pointers (ksk, bsk, pfpksk)")
     ctx = C.c_void_p()
     check(lib().tae_context_create_raw(param_set, device, ptrs[0], ptrs[1], ptrs[2], mem, C.byref(ctx)))
     return FheContext(ctx.value, param_set)
@@ -316,7 +387,7 @@ def save_keys(path, param_set: int, client_key: "ClientKey | None" = None, serve
     keys (ksk, bsk, pfpksk) as returned by generate_keys_raw."""
     ptrs = [None, None, None]
     if server_keys is not None:
-        arrs = [np.ascontiguousarray(k, dtype=np.uint64) for k in server_keys]
+        arrs = _checked_key_arrays(param_set, server_keys)
         ptrs = [a.ctypes.data_as(C.c_void_p) for a in arrs]
     check(lib().tae_keys_save(os.fsencode(path), param_set, client_key._h if client_key else None, *ptrs))
 
@@ -335,9 +406,7 @@ def load_keys(path, client: bool = True, server: bool = True):
     client, server = client and has_ck, server and has_sk
     ptrs, arrs = [None, None, None], None
     if server:
-        sizes = [C.c_size_t() for _ in range(3)]
-        check(lib().tae_server_key_sizes(param_set, *[C.byref(s) for s in sizes]))
-        arrs = tuple(np.empty(s.value, dtype=np.uint64) for s in sizes)
+        arrs = tuple(np.empty(n, dtype=np.uint64) for n in server_key_sizes(param_set))
         ptrs = [a.ctypes.data_as(C.c_void_p) for a in arrs]
     ck = C.c_void_p()
     check(lib().tae_keys_load(os.fsencode(path), C.byref(ck) if client else None, *ptrs))
