@@ -1,5 +1,9 @@
 #!/bin/bash
+# GPU-box: time the PBS stage (scripts/debug/time_pbs.py) for every debug variant library in
+# tfhe-aes-2_amd/dbg/*.so (built by build_variants.sh), twice each in alternating order.
 cd "$(dirname "$0")/../.."
-for lib in tfhe-aes-2_amd/dbg/*.so; do
-  TAE_LIB_PATH=$PWD/$lib timeout -k 10 200 python scripts/debug/time_pbs.py 2>&1 | tail -1 || exit 1
+for pass in 1 2; do
+  for lib in tfhe-aes-2_amd/dbg/*.so; do
+    TAE_LIB_PATH=$PWD/$lib timeout -k 10 200 python scripts/debug/time_pbs.py 2>&1 | tail -1 || exit 1
+  done
 done

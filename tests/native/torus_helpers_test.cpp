@@ -20,6 +20,16 @@ static int fails = 0;
 static void check_ft(double x) {
     const uint64_t a = tae::from_torus_bits(x), b = or_from_torus(x);
     if (a != b && fails++ < 10) printf("from_torus(%a): got %016llx want %016llx\n", x, (unsigned long long)a, (unsigned long long)b);
+    // the kernels' fast path: acc + from_torus(x) whenever it accepts x (and it must accept every
+    // |x| in [2^-12, 2^52))
+    const uint64_t acc0 = 0x0123456789abcdefull ^ (uint64_t)(int64_t)(x * 7);
+    uint64_t acc = acc0;
+    const bool ok = tae::torus_acc_fast(x, acc);
+    const double ax = std::fabs(x);
+    if (ok ? acc != acc0 + b : (ax >= 0x1p-12 && ax < 0x1p52)) {
+        if (fails++ < 10) printf("torus_acc_fast(%a): ok %d got %016llx want %016llx\n", x, (int)ok,
+                                 (unsigned long long)(acc - acc0), (unsigned long long)b);
+    }
 }
 
 template <int LEV, int B>
@@ -69,7 +79,10 @@ int main(int argc, char **argv) {
     // from_torus: magnitudes across every exponent that matters, exact halves, integers, zeros
     const double specials[] = {0.0, -0.0, 0.5, -0.5, 1.5, -1.5, 2.5, -2.5, 1.0, -1.0, 0x1p-64, -0x1p-64, 0x1p-65,
                                -0x1p-65, 0x1.8p-65, -0x1.8p-65, 0x1p-66, 0x1p52, -0x1p52, 0x1p53 + 2, 0x1p70, -0x1p70,
-                               0x1p-1022, 0x1p-1074, 1e300, -1e300, 0.25, -0.25, 0x1.fffffffffffffp-2, -0x1.fffffffffffffp-2};
+                               0x1p-1022, 0x1p-1074, 1e300, -1e300, 0.25, -0.25, 0x1.fffffffffffffp-2, -0x1.fffffffffffffp-2,
+                               0x1p-12, -0x1p-12, 0x1.fffffffffffffp-13, -0x1.fffffffffffffp-13, 0x1.fffffffffffffp51,
+                               -0x1.fffffffffffffp51, 0x1p51 + 0.5, -(0x1p51 + 0.5), -(0x1p40 + 0.5), -0.5 - 0x1p30,
+                               -0x1p-64, 0x1.8p-12, -0x1.8p-12, 1.0 / 3.0, -1.0 / 3.0};
     for (double x : specials) check_ft(x);
     for (long i = 0; i < n; i++) {
         const uint64_t r = rng();

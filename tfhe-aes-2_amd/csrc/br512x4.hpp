@@ -1,19 +1,23 @@
-// Batched blind rotation for N = 512, k = 4 with FOUR waves per SIMD: 1024-thread workgroups.
+// Batched blind rotation for N = 512, k = 4 (params_sqrd_lvl_64) with FOUR waves per SIMD:
+// 1024-thread workgroups, C = 3 ciphertexts each, ACC and one level of spectra in LDS, every GGSW
+// value loaded from L2 feeding three accumulators.
 //
-// Same work split as br512x2.hpp (C = 3 ciphertexts per workgroup, ACC and one level of spectra in
-// LDS, GGSW values shared by the three accumulators of a Fourier position), but every FFT job
-// (ciphertext, polynomial) is one whole wave: lane (u, r) = (lane & 15, lane >> 4) holds the four
-// points x[r + 4 i] of column (or row) u of the 16 x 16 FFT.  A DFT16 then runs as
+// Every FFT job (ciphertext, polynomial) is one whole wave: lane (u, r) = (lane & 15, lane >> 4)
+// holds the four points x[r + 4 i] of column (or row) u of the 16 x 16 FFT.  A DFT16 runs as
 //   DFT4 over i in registers -> W16^{r k1} -> 4 x 4 transpose across the lanes u, u+16, u+32, u+48
-//   (two v_permlane32_swap and two v_permlane16_swap per complex pair, semantics probed by
-//   scripts/probes/permlane_swap.hip) -> DFT4 over r,
+//   -> DFT4 over r,
 // every output getting the oracle's DFT16 operation sequence (tfhe_oracle.c); the W16^0 / W16^4
 // factors are generic products with exact (1, 0) / (0, -1) and change nothing but signs of zeros.
-// 16 waves (15 jobs + 1 idle) give the SIMDs four waves each to hide LDS, GGSW-load and f64
-// latencies; registers are held under 128 per lane.  The MAC splits the 15 (q, ct) accumulators of
-// a Fourier position 4/4/4/3 over four 256-thread groups (one wave of each group per SIMD).
-// Lane (u, r) of a job decomposes and updates the ACC coefficients j = u + 16 r + 64 i (+ 256), so
-// each LDS access of a wave touches 64 consecutive coefficients.
+// The kernel is bound by VALU issue (scripts/probes/valu_rates.hip: one wave issues a VALU op at
+// most every ~14 cycles, four waves keep the SIMD near its ~6-cycle f64 rate): the permlane
+// transposes cost ~7% of the launch and moving them to LDS costs more (+15%, the MAC, table and
+// pass traffic already keeps LDS about half busy); the torus conversion takes the integer fast path
+// (fft_device.hpp torus_acc_fast).
+// 16 waves (15 jobs + 1 idle) give the SIMDs four waves each; registers are held under 128 per
+// lane.  The MAC splits the 15 (q, ct) accumulators of a Fourier position 4/4/4/3 over four
+// 256-thread groups (one wave of each group per SIMD).  Lane (u, r) of a job decomposes and
+// updates the ACC coefficients j = u + 16 r + 64 i (+ 256), so each LDS access of a wave touches
+// 64 consecutive coefficients.
 #pragma once
 #include "br512.hpp"
 
@@ -24,11 +28,11 @@ using br512::BUF_STRIDE;
 using br512::K1;
 using br512::lds_sync;
 using br512::M;
+using br512::mac_pos;
 using br512::N;
 using br512::pidx;
-using br512::u32x4;
-using br512::mac_pos;
 using br512::swap16;
+using br512::u32x4;
 using br512::wave_sync;
 
 constexpr int C = 3, JOBS = C * K1, THREADS = 1024;
@@ -37,40 +41,27 @@ constexpr int C = 3, JOBS = C * K1, THREADS = 1024;
 // it completes parts of the phase, so the SIMD arbiter favours the waves that are behind and the
 // four waves of a SIMD reach the next barrier together (oldest-first arbitration otherwise starves
 // the youngest wave, whose tail then runs alone with its latencies exposed).
-#define DBG_SYNC() br512::lds_sync()
-#ifndef TAE_X4_NORR
 #define PRIO(n) __builtin_amdgcn_s_setprio(n)
-#else
-#define PRIO(n) \
-    do {        \
-    } while (0)
-#endif
 
-// TAE_X4_PROF (debug builds only): per-phase cycle sums of every wave of workgroup 0, printed at exit
+// TAE_X4_PROF (debug builds only): per-phase cycle sums (s_memtime) of every wave of one workgroup,
+// printed at exit: 0 decomposition, 1 pass A, 2 pass B, 3 barrier after the FFTs, 4 MAC, 5 barrier
+// after the MAC, 6 MAC store + barrier, 7 pass B^-1, 8 pass A^-1 + ACC update, 9 end-of-step wait.
 #ifdef TAE_X4_PROF
 #define PROF_DECL uint64_t prof_[10] = {0}, prof_t_ = clock64();
-#define PROF_T(i)                          \
-    do {                                   \
-        asm volatile("" ::: "memory");     \
-        const uint64_t now_ = clock64();   \
-        prof_[i] += now_ - prof_t_;        \
-        prof_t_ = now_;                    \
-    } while (0)
-#define PROF_SYNC(i)                                                   \
-    do {                                                               \
-        PROF_T(i);                                                     \
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");            \
-        PROF_T(9);                                                     \
-        DBG_SYNC();                                                    \
-        PROF_T(8);                                                     \
+#define PROF_T(i)                        \
+    do {                                 \
+        asm volatile("" ::: "memory");   \
+        const uint64_t now_ = clock64(); \
+        prof_[i] += now_ - prof_t_;      \
+        prof_t_ = now_;                  \
     } while (0)
 #else
 #define PROF_DECL
 #define PROF_T(i) \
     do {          \
     } while (0)
-#define PROF_SYNC(i) DBG_SYNC()
 #endif
+
 constexpr int ACC_STRIDE = N;
 
 __device__ __forceinline__ void swap32(cplx &x, cplx &y) {
@@ -91,7 +82,7 @@ __device__ __forceinline__ void swap32(cplx &x, cplx &y) {
 
 // DFT16 over the lanes (u, 0..3) of a row group: in v[i] = x[r + 4 i], out v[k2] = X[r + 4 k2];
 // tw[k1 - 1] = W16^{r k1} (forward values).  Stage-1 outputs M[r][k1] are transposed to
-// M[0..3][r]: swap32 on k1 bit 1 vs r bit 1, then swap16 on bit 0.
+// M[0..3][r]: swap32 on k1 bit 1 vs r bit 1, then swap16 on bit 0.  (br512lat's register form.)
 template <bool INV>
 __device__ __forceinline__ void dft16x4(cplx *v, const cplx *tw) {
     dft4<INV>(v[0], v[1], v[2], v[3]);
@@ -222,6 +213,7 @@ __global__ void __launch_bounds__(THREADS, 1)
     cplx accr[4];
     cplx gv[K1 * 2];
     const cplx *my_w16 = s_w16 + 3 * r;
+    cplx *jbuf = buf + jb * BUF_STRIDE;  // this job's spectrum
     PROF_DECL
     for (int step = 0; step < steps; step++) {
         int e, gstep;
@@ -267,21 +259,11 @@ __global__ void __launch_bounds__(THREADS, 1)
                 const uint64_t v0 = poly[ph], v1 = poly[ph ^ M];
                 const uint64_t p0 = poly[j], p1 = poly[j + M];
                 const uint64_t x0 = (v0 ^ m0) - (p0 + m0), x1 = (v1 ^ m1) - (p1 + m1);
-#ifdef TAE_DBG_NODEC
-                for (int l = 0; l < LEV; l++) dig[l][i] = ((uint32_t)x0 & 0x7ff) | (((uint32_t)x1 & 0x7ff) << 16);
-#elif defined(TAE_DEC_SCALAR)
-                uint32_t d0[LEV], d1[LEV];
-                decompose16<LEV>(x0, BLOG, d0);
-                decompose16<LEV>(x1, BLOG, d1);
-#pragma unroll
-                for (int l = 0; l < LEV; l++) dig[l][i] = d0[l] | (d1[l] << 16);
-#else
                 // both halves at once with 16-bit SIMD ops (fft_device.hpp decompose16p)
                 uint32_t dp[LEV];
                 decompose16p<LEV, BLOG>(x0, x1, dp);
 #pragma unroll
                 for (int l = 0; l < LEV; l++) dig[l][i] = dp[l];
-#endif
             }
         }
 #pragma unroll
@@ -291,11 +273,7 @@ __global__ void __launch_bounds__(THREADS, 1)
 
 #pragma unroll
         for (int lev = LEV; lev >= 1; lev--) {
-#if defined(TAE_DBG_NOGLOAD)
-            if (lev == LEV) load_level(lev);
-#elif !defined(TAE_X4_G_MID) && !defined(TAE_X4_G_LATE)
             load_level(lev);
-#endif
             // pass A (column u): twist, DFT16 over m = r + 4 i, W_M^{u k} -> LDS position u + 16 k
             if (fjob) {
                 cplx v[4];
@@ -311,48 +289,38 @@ __global__ void __launch_bounds__(THREADS, 1)
                 }
                 dft16x4<false>(v, my_w16);
                 if (lev == LEV) PRIO(1); else PRIO(2);
-                cplx *dst = buf + jb * BUF_STRIDE;
 #pragma unroll
                 for (int k2 = 0; k2 < 4; k2++) {
                     const int k = r + 4 * k2;
-                    dst[pidx(u + 16 * k)] = cmul(v[k2], s_twa[16 * k + u]);
+                    jbuf[pidx(u + 16 * k)] = cmul(v[k2], s_twa[16 * k + u]);
                 }
             }
             wave_sync();
             PRIO(1);
-#ifdef TAE_X4_G_MID
-            load_level(lev);
-#endif
             PROF_T(1);
             // pass B (row u): DFT16 over positions 16 u + r + 4 i, in place
             if (fjob) {
-                cplx *base = buf + jb * BUF_STRIDE;
                 cplx v[4];
 #pragma unroll
-                for (int i = 0; i < 4; i++) v[i] = base[pidx(16 * u + r + 4 * i)];
+                for (int i = 0; i < 4; i++) v[i] = jbuf[pidx(16 * u + r + 4 * i)];
                 dft16x4<false>(v, my_w16);
                 PRIO(0);
 #pragma unroll
-                for (int k2 = 0; k2 < 4; k2++) base[pidx(16 * u + r + 4 * k2)] = v[k2];
+                for (int k2 = 0; k2 < 4; k2++) jbuf[pidx(16 * u + r + 4 * k2)] = v[k2];
             }
-#ifdef TAE_X4_G_LATE
-            load_level(lev);
-#endif
-            PROF_SYNC(2);
+            PROF_T(2);
+            lds_sync();
+            PROF_T(3);
             PRIO(3);
-#ifndef TAE_DBG_NOMAC
             switch (grp) {
             case 0: mac_level<0>(buf, pidx(pos), accr, gv); break;
             case 1: mac_level<1>(buf, pidx(pos), accr, gv); break;
             case 2: mac_level<2>(buf, pidx(pos), accr, gv); break;
             default: mac_level<3>(buf, pidx(pos), accr, gv); break;
             }
-#endif
-#ifdef TAE_DBG_NOBAR3
-            wave_sync();
-#else
-            PROF_SYNC(3);
-#endif
+            PROF_T(4);
+            lds_sync();
+            PROF_T(5);
             PRIO(3);
         }
         // ---- inverse FFT of the MAC results, accumulated into ACC ----
@@ -362,27 +330,26 @@ __global__ void __launch_bounds__(THREADS, 1)
         case 2: mac_store<2>(buf, pidx(pos), accr); break;
         default: mac_store<3>(buf, pidx(pos), accr); break;
         }
-        PROF_SYNC(4);
+        lds_sync();
+        PROF_T(6);
         PRIO(3);
         if (fjob) {  // pass B^-1 (row u)
-            cplx *base = buf + jb * BUF_STRIDE;
             cplx v[4];
 #pragma unroll
-            for (int i = 0; i < 4; i++) v[i] = base[pidx(16 * u + r + 4 * i)];
+            for (int i = 0; i < 4; i++) v[i] = jbuf[pidx(16 * u + r + 4 * i)];
             dft16x4<true>(v, my_w16);
 #pragma unroll
-            for (int k2 = 0; k2 < 4; k2++) base[pidx(16 * u + r + 4 * k2)] = v[k2];
+            for (int k2 = 0; k2 < 4; k2++) jbuf[pidx(16 * u + r + 4 * k2)] = v[k2];
         }
         wave_sync();
+        PROF_T(7);
         PRIO(3);
-        PROF_T(5);
         if (fjob) {  // pass A^-1 (column u): conj(W_M^{u kk}), DFT16^-1 over kk, untwist, from_torus, ACC +=
-            const cplx *src = buf + jb * BUF_STRIDE;
             cplx v[4];
 #pragma unroll
             for (int i = 0; i < 4; i++) {
                 const int kk = r + 4 * i;
-                v[i] = cmul(src[pidx(u + 16 * kk)], cconj(s_twa[16 * kk + u]));
+                v[i] = cmul(jbuf[pidx(u + 16 * kk)], cconj(s_twa[16 * kk + u]));
             }
             dft16x4<true>(v, my_w16);
             uint64_t *poly = acc + jb * ACC_STRIDE;
@@ -390,25 +357,28 @@ __global__ void __launch_bounds__(THREADS, 1)
             for (int k2 = 0; k2 < 4; k2++) {
                 const int j = ll + 64 * k2;  // m = r + 4 k2 -> j = u + 16 m
                 const cplx t = cmul(v[k2], s_utw[j]);
-#ifdef TAE_DBG_NOTAIL
-                poly[j] += (uint64_t)__double_as_longlong(t.re);
-                poly[j + M] += (uint64_t)__double_as_longlong(t.im);
-#else
-                poly[j] += from_torus_bits(t.re);
-                poly[j + M] += from_torus_bits(t.im);
-#endif
+                uint64_t a0 = poly[j], a1 = poly[j + M];
+                const bool f0 = torus_acc_fast(t.re, a0), f1 = torus_acc_fast(t.im, a1);
+                if (!(f0 && f1)) {  // zeros and out-of-range magnitudes (rare; the wave skips it otherwise)
+                    a0 = poly[j] + from_torus_bits(t.re);
+                    a1 = poly[j + M] + from_torus_bits(t.im);
+                }
+                poly[j] = a0;
+                poly[j + M] = a1;
             }
         }
         wave_sync();
+        PROF_T(8);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        PROF_T(6);
+        PROF_T(9);
     }
 #ifdef TAE_X4_PROF
-    if (blockIdx.x == 0 && lane == 0)
-        printf("x4prof wave %2d: dec %llu passA %llu passB %llu mac %llu store %llu invB %llu invA %llu bar %llu lgkm %llu\n",
+    if (blockIdx.x == 100 && lane == 0)
+        printf("x4prof wave %2d: dec %llu passA %llu passB %llu barF %llu mac %llu barM %llu store %llu invB %llu invA %llu end %llu\n",
                jb, (unsigned long long)prof_[0], (unsigned long long)prof_[1], (unsigned long long)prof_[2],
                (unsigned long long)prof_[3], (unsigned long long)prof_[4], (unsigned long long)prof_[5],
-               (unsigned long long)prof_[6], (unsigned long long)prof_[8], (unsigned long long)prof_[9]);
+               (unsigned long long)prof_[6], (unsigned long long)prof_[7], (unsigned long long)prof_[8],
+               (unsigned long long)prof_[9]);
 #endif
     lds_sync();  // sample extraction reads every job's ACC
     for (int ct = 0; ct < nct; ct++) {
