@@ -12,5 +12,5 @@ timeout -k 10 200 python scripts/debug/time_pbs.py > gpurun_out/pbs_check_time.l
 tail -2 gpurun_out/pbs_check_time.log
 if [ "${BENCH:-1}" = "1" ]; then
   timeout -k 10 300 python bench.py --steps 2 --warmup 1 --cpu-baseline off --model8-leg off > gpurun_out/pbs_check_bench.json 2> gpurun_out/pbs_check_bench.err || { tail -20 gpurun_out/pbs_check_bench.err; exit 1; }
-  python3 -c "import json; d=json.load(open('gpurun_out/pbs_check_bench.json')); r=d['roofline']; print('value', round(d['value'],2), 'blocks/s; pbs kernel', round(r['avg_launch_ms'],2), 'ms frac', round(r['frac'],3), 'stage', d['stage_ms_per_step'], 'single', d['single_block']['s_per_block'])"
+  python3 -c "import json; d=json.load(open('gpurun_out/pbs_check_bench.json')); r=d['roofline']; print('value', round(d['value'],2), 'blocks/s; pbs kernel', round(r['avg_launch_ms'],2), 'ms frac', round(r['frac'],3), 'stage', d['stage_ms_per_step'], 'single', d['single_block']['s_per_block'], d['single_block'].get('stage_ms'))"
 fi

@@ -1,13 +1,20 @@
 // Latency-oriented blind rotation for N = 512, k = 4 (small batches: one AES block is 128 bits):
 // ONE ciphertext per 1024-thread workgroup, and the decomposition LEVELS run in parallel instead
 // of one after another.  Wave jb < LEV * (k+1) owns FFT job (level jb / (k+1) + 1, polynomial
-// jb % (k+1)), so a CMux step is
-//   forward FFT of all LEV * (k+1) digit polynomials                    (one wave each) | barrier
-//   MAC of all levels: thread task (q, position) = 15 complex terms     -> out[q]       | barrier
-//   inverse FFT of the k+1 outputs (waves 0..k), ACC +=, and the next step's decomposition of
-//   that polynomial (all levels once; the finer levels to LDS for their FFT waves)       | barrier
-// three barriers per step instead of the 2 LEV + 1 of br512x4 (which spends them on three
-// ciphertexts per workgroup for throughput).  The FFT jobs reuse br512x4's 4-lane DFT16
+// jb % (k+1)).  A CMux step is four barrier-separated phases:
+//   D  decomposition of the rotated difference ACC * X^e - ACC of all k+1 polynomials, all levels
+//      at once, spread over all 16 waves (coefficient pairs (p, j), j < N/2), digits -> LDS
+//   F  forward FFT of all LEV * (k+1) digit polynomials (one wave each); the MAC's GGSW loads are
+//      issued before the FFT work so that they land during it
+//   M  MAC: thread chain (q, position) = 15 complex terms -> out[q]; 1280 chains on 1024 threads,
+//      waves 0-3 run two chains (q = 0 and 4) of one position, sharing its spectrum reads (holding
+//      the next level's rows in registers as well spills: 80 VGPRs of GGSW values alone; the level
+//      loop stays rolled, else the scheduler hoists all three levels' loads and spills)
+//   I  inverse FFT of the k+1 outputs (waves 0..k), untwist, torus conversion, ACC +=; the other
+//      waves issue the L2 prefetch of the GGSW rows two steps ahead, so that no phase waits on it
+// The per-phase profile of the previous layout (TAE_LAT_PROF) had the decomposition inside the
+// inverse phase (five waves, single-wave issue rate) and three dependent GGSW load rounds per MAC
+// chain behind the vmcnt of the prefetch loads.  The FFT jobs use br512x4's 4-lane DFT16
 // (dft16x4), and every output keeps the oracle's operation order (levels descending, rows
 // ascending, the same fma chain): results are bit-identical to br512x4 and the oracle.  Only the
 // PBS flavour (homomorphic_shift_boolean) is instantiated.  Each workgroup loads the GGSW rows for
@@ -24,10 +31,10 @@ using br512::BUF_STRIDE;
 using br512::K1;
 using br512::lds_sync;
 using br512::M;
+using br512::mac_pos;
 using br512::N;
 using br512::pidx;
 using br512::u32x4;
-using br512::mac_pos;
 using br512::wave_sync;
 using br512x4::dft16x4;
 
@@ -65,7 +72,7 @@ __global__ void __launch_bounds__(THREADS, 1)
     cplx *s_twa = s_tw + M;                                         // [16 a + b] = W_M^{a b}
     cplx *s_utw = s_twa + M;                                        // conj(twist) 2^-8 (exact)
     cplx *s_w16 = s_utw + M;                                        // [r][3]: W16^{r k1}
-    uint32_t *s_dig = reinterpret_cast<uint32_t *>(s_w16 + 12);     // [LEV-1][K1][4][64] digits
+    uint32_t *s_dig = reinterpret_cast<uint32_t *>(s_w16 + 12);     // [LEV][K1][N/2] packed digit pairs
     const long ct = blockIdx.x;
     if (ct >= B) return;  // whole workgroup
     const int tid = threadIdx.x;
@@ -99,107 +106,79 @@ __global__ void __launch_bounds__(THREADS, 1)
     const size_t ggsw_sz = (size_t)LEV * K1 * K1 * M;
     const uint32_t gbytes = (uint32_t)((size_t)n * ggsw_sz * sizeof(cplx));
     const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc((void *)bsk, (short)0, gbytes, 0x00020000);
-    // MAC tasks (q, position): q = tid / 256 for every thread, and q = 4 also for waves 12-15 (one
-    // wave per SIMD, so each SIMD runs five task-waves)
-    const int pos0 = mac_pos(tid & (M - 1)), q0 = tid >> 8;
+    // MAC chains: thread tid runs chain (q = tid >> 8, pos); threads tid < 256 also run (q = 4, pos)
+    const int pos = mac_pos(tid & (M - 1)), qa = tid >> 8;
+    const bool two = tid < M;
+    const int goff = pos * (int)sizeof(cplx);
     const cplx *my_w16 = s_w16 + 3 * r;
     int ll = lane;
     asm volatile("" : "+v"(ll));
 
-    // MAC task (q, pos): 15 complex terms, levels descending, rows ascending, the oracle's fma chain
-    // (the GGSW rows are L2 hits thanks to the prefetch below)
-    auto mac_task = [&](int q, int pos, int gstep) {
-        double re = 0.0, im = 0.0;
-#pragma unroll
-        for (int lev = LEV; lev >= 1; lev--) {
-            cplx g[K1];
-#pragma unroll
-            for (int p = 0; p < K1; p++) {
-                const int soff = gstep + (((lev - 1) * K1 + p) * K1 + q) * M * (int)sizeof(cplx);
-                const u32x4 rv = __builtin_amdgcn_raw_buffer_load_b128(grs, pos * (int)sizeof(cplx), soff, 0);
-                __builtin_memcpy(&g[p], &rv, sizeof(cplx));
-            }
-#pragma unroll
-            for (int p = 0; p < K1; p++) {
-                const cplx x = buf[((lev - 1) * K1 + p) * BUF_STRIDE + pidx(pos)];
-                re = fma(x.re, g[p].re, re);
-                re = fma(-x.im, g[p].im, re);
-                im = fma(x.re, g[p].im, im);
-                im = fma(x.im, g[p].re, im);
-            }
-        }
-        obuf[q * BUF_STRIDE + pidx(pos)] = cplx{re, im};
+    // GGSW value (lev, p, q) of this thread's position at step offset gstep: the wave-uniform part of
+    // the offset goes to the scalar operand, q (per thread for chain a) to the vector one
+    auto gload = [&](int gstep, int lev, int p, int q, bool qvec) {
+        const int soff = gstep + (((lev - 1) * K1 + p) * K1 + (qvec ? 0 : q)) * M * (int)sizeof(cplx);
+        const int voff = goff + (qvec ? q * M * (int)sizeof(cplx) : 0);
+        const u32x4 rv = __builtin_amdgcn_raw_buffer_load_b128(grs, voff, soff, 0);
+        cplx g;
+        __builtin_memcpy(&g, &rv, sizeof(cplx));
+        return g;
     };
 
-    // L2 prefetch of the GGSW rows two steps ahead: one dword per 128-byte line (the batch is small,
-    // so a step's 307 KB are otherwise first touched -- from HBM -- by the MAC that needs them).  A
-    // prefetch's value is consumed (asm register use) one step later, when it has long returned.
+    // L2 prefetch of the GGSW rows two steps ahead, one dword per 128-byte line, issued by the waves
+    // that are idle during the inverse phase; a prefetch's value is consumed (asm register use) a step
+    // later, when it has long returned, so it never holds back a vmcnt wait of the MAC.  Every
+    // workgroup reads the same rows, and workgroups b and b + 8 share an XCD (and its L2: blocks are
+    // dealt round-robin over the 8 XCDs), so the workgroups of one XCD split the lines between them.
+    constexpr int PFW = THREADS - K1 * 64;  // prefetching threads (waves K1..15)
     constexpr int GLINES = (int)((ggsw_sz * sizeof(cplx) + 127) / 128);
-    constexpr int PF = (GLINES + THREADS - 1) / THREADS;
-    uint32_t pf_prev[PF], pf_cur[PF];
+    constexpr int PF = (GLINES + PFW - 1) / PFW;
+    const int xg = (int)(ct & 7), xrank = (int)(ct >> 3), xcnt = (int)((B - xg + 7) >> 3);
+    const int pf_n = (GLINES + xcnt - 1) / xcnt;  // lines of this workgroup: xrank + xcnt * i
+    uint32_t pf_prev[PF];
 #pragma unroll
     for (int i = 0; i < PF; i++) pf_prev[i] = 0;
-    // Decomposition of polynomial jb (waves 0..k, the level-1 jobs, which also own output q = jb of
-    // the inverse FFT and so update ACC polynomial jb): all levels at once, once per polynomial;
-    // level 1 stays in registers, the finer levels go to LDS for the waves of those jobs.
-    uint32_t mydig[4];
-    auto decompose_poly = [&](int e) {
-        const uint64_t *poly = acc + jb * N;
-        const int bt = ll - e;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int j = ll + 64 * i;
-            const int t = (bt + 64 * i) & (2 * N - 1);
-            const int ph = t & (N - 1);
-            const uint64_t m0 = (uint64_t)(int64_t)((t << 22) >> 31);
-            const uint64_t m1 = (uint64_t)(int64_t)(((t + M) << 22) >> 31);
-            const uint64_t v0 = poly[ph], v1 = poly[ph ^ M];
-            const uint64_t p0 = poly[j], p1 = poly[j + M];
-            const uint64_t x0 = (v0 ^ m0) - (p0 + m0), x1 = (v1 ^ m1) - (p1 + m1);
-            uint32_t dp[LEV];
-            decompose16p<LEV, BLOG>(x0, x1, dp);
-            mydig[i] = dp[0];
-#pragma unroll
-            for (int l = 1; l < LEV; l++) s_dig[(((l - 1) * K1 + jb) * 4 + i) * 64 + ll] = dp[l];
-        }
-    };
-    if (jb < K1 && n > 0) decompose_poly(mod_switch(in[0], LOGN) % (2 * N));
-    lds_sync();
+
     LPROF_DECL
     for (int step = 0; step < n; step++) {
         const int gstep = step * (int)(ggsw_sz * sizeof(cplx));
-#ifndef TAE_LAT_NOPF
-        if (step + 2 < n) {
+        // ---- D: decomposition of the rotated difference, pairs (p, j) and (p, j + N/2) ----
+        {
+            const int e = mod_switch(in[step], LOGN) % (2 * N);
+            for (int t = tid; t < K1 * M; t += THREADS) {
+                const int p = t >> 8, j = t & (M - 1);
+                const uint64_t *poly = acc + p * N;
+                const int tt = (j - e) & (2 * N - 1);  // coefficient j of ACC * X^e: entry tt of [ACC, -ACC]
+                const int ph = tt & (N - 1);
+                const uint64_t m0 = (uint64_t)(int64_t)((tt << 22) >> 31);
+                const uint64_t m1 = (uint64_t)(int64_t)(((tt + M) << 22) >> 31);
+                const uint64_t v0 = poly[ph], v1 = poly[ph ^ M];
+                const uint64_t p0 = poly[j], p1 = poly[j + M];
+                const uint64_t x0 = (v0 ^ m0) - (p0 + m0), x1 = (v1 ^ m1) - (p1 + m1);
+                uint32_t dp[LEV];
+                decompose16p<LEV, BLOG>(x0, x1, dp);
 #pragma unroll
-            for (int i = 0; i < PF; i++) {
-                const int line = tid + THREADS * i;
-                pf_cur[i] = line < GLINES ? __builtin_amdgcn_raw_buffer_load_b32(
-                                                grs, line * 128, gstep + 2 * (int)(ggsw_sz * sizeof(cplx)), 0)
-                                          : 0u;
+                for (int l = 0; l < LEV; l++) s_dig[(l * K1 + p) * M + j] = dp[l];
             }
         }
+        LPROF(0);
+        lds_sync();
+        LPROF(1);
+        // ---- F: forward FFTs; this thread's first-level GGSW values are loaded meanwhile ----
+        cplx ga[K1], gb[K1];
 #pragma unroll
-        for (int i = 0; i < PF; i++) {
-            asm volatile("" ::"v"(pf_prev[i]));
-            pf_prev[i] = pf_cur[i];
+        for (int p = 0; p < K1; p++) ga[p] = gload(gstep, LEV, p, qa, true);
+        if (two) {
+#pragma unroll
+            for (int p = 0; p < K1; p++) gb[p] = gload(gstep, LEV, p, K1 - 1, false);
         }
-#endif
         if (fjob) {
-            uint32_t dig[4];
-            if (jb < K1) {  // level 1: computed by this wave at the end of the previous step
-#pragma unroll
-                for (int i = 0; i < 4; i++) dig[i] = mydig[i];
-            } else {
-#pragma unroll
-                for (int i = 0; i < 4; i++) dig[i] = s_dig[(((jlev - 2) * K1 + jp) * 4 + i) * 64 + ll];
-            }
-            LPROF(0);
-            // pass A (column u): twist, DFT16 over m = r + 4 i, W_M^{u k} -> position u + 16 k
             cplx *dst = buf + jb * BUF_STRIDE;
             cplx v[4];
 #pragma unroll
             for (int i = 0; i < 4; i++) {
-                const double a0 = br512::lo16(dig[i]), a1 = br512::hi16(dig[i]);
+                const uint32_t d = s_dig[((jlev - 1) * K1 + jp) * M + ll + 64 * i];
+                const double a0 = br512::lo16(d), a1 = br512::hi16(d);
                 const cplx tw = s_tw[ll + 64 * i];
                 v[i] = {fma(a0, tw.re, -(a1 * tw.im)), fma(a0, tw.im, a1 * tw.re)};
             }
@@ -210,7 +189,6 @@ __global__ void __launch_bounds__(THREADS, 1)
                 dst[pidx(u + 16 * kq)] = cmul(v[k2], s_twa[16 * kq + u]);
             }
             wave_sync();
-            LPROF(1);
             // pass B (row u): DFT16 over positions 16 u + r + 4 i, in place
 #pragma unroll
             for (int i = 0; i < 4; i++) v[i] = dst[pidx(16 * u + r + 4 * i)];
@@ -221,12 +199,44 @@ __global__ void __launch_bounds__(THREADS, 1)
         LPROF(2);
         lds_sync();
         LPROF(3);
-        mac_task(q0, pos0, gstep);
-        if (tid >= 3 * M) mac_task(K1 - 1, pos0, gstep);
+        // ---- M: MAC chains, levels descending, rows ascending, the oracle's fma chain; a level's
+        // GGSW values below the first are loaded at its start (L2 hits: every workgroup reads the
+        // same rows this step, and the prefetch waves pulled them in two steps earlier) ----
+        {
+            double ar = 0.0, ai = 0.0, br = 0.0, bi = 0.0;
+#pragma unroll 1
+            for (int lev = LEV; lev >= 1; lev--) {
+                if (lev < LEV) {
+#pragma unroll
+                    for (int p = 0; p < K1; p++) ga[p] = gload(gstep, lev, p, qa, true);
+                    if (two) {
+#pragma unroll
+                        for (int p = 0; p < K1; p++) gb[p] = gload(gstep, lev, p, K1 - 1, false);
+                    }
+                }
+#pragma unroll
+                for (int p = 0; p < K1; p++) {
+                    const cplx x = buf[((lev - 1) * K1 + p) * BUF_STRIDE + pidx(pos)];
+                    ar = fma(x.re, ga[p].re, ar);
+                    ar = fma(-x.im, ga[p].im, ar);
+                    ai = fma(x.re, ga[p].im, ai);
+                    ai = fma(x.im, ga[p].re, ai);
+                    if (two) {
+                        br = fma(x.re, gb[p].re, br);
+                        br = fma(-x.im, gb[p].im, br);
+                        bi = fma(x.re, gb[p].im, bi);
+                        bi = fma(x.im, gb[p].re, bi);
+                    }
+                }
+            }
+            obuf[qa * BUF_STRIDE + pidx(pos)] = cplx{ar, ai};
+            if (two) obuf[(K1 - 1) * BUF_STRIDE + pidx(pos)] = cplx{br, bi};
+        }
         LPROF(4);
         lds_sync();
         LPROF(5);
-        if (jb < K1) {  // inverse FFT of output q = jb, ACC +=
+        // ---- I: inverse FFT of output q = jb, ACC += (waves 0..k); prefetch (the other waves) ----
+        if (jb < K1) {
             cplx *base = obuf + jb * BUF_STRIDE;
             cplx v[4];
 #pragma unroll
@@ -246,19 +256,36 @@ __global__ void __launch_bounds__(THREADS, 1)
             for (int k2 = 0; k2 < 4; k2++) {
                 const int j = ll + 64 * k2;
                 const cplx t = cmul(v[k2], s_utw[j]);
-                poly[j] += from_torus_bits(t.re);
-                poly[j + M] += from_torus_bits(t.im);
+                uint64_t a0 = poly[j], a1 = poly[j + M];
+                const bool f0 = torus_acc_fast(t.re, a0), f1 = torus_acc_fast(t.im, a1);
+                if (!(f0 && f1)) {  // zeros and out-of-range magnitudes (rare)
+                    a0 = poly[j] + from_torus_bits(t.re);
+                    a1 = poly[j + M] + from_torus_bits(t.im);
+                }
+                poly[j] = a0;
+                poly[j + M] = a1;
             }
-            wave_sync();
-            if (step + 1 < n) decompose_poly(mod_switch(in[step + 1], LOGN) % (2 * N));
+        } else if (step + 2 < n) {
+#pragma unroll
+            for (int i = 0; i < PF; i++) {
+                asm volatile("" ::"v"(pf_prev[i]));
+                const int k = (tid - K1 * 64) + PFW * i, line = xrank + xcnt * k;
+                if (PFW * i < pf_n)  // wave-uniform: no empty instructions for the later slots
+                    pf_prev[i] = k < pf_n && line < GLINES
+                                     ? __builtin_amdgcn_raw_buffer_load_b32(
+                                           grs, line * 128, gstep + 2 * (int)(ggsw_sz * sizeof(cplx)), 0)
+                                     : 0u;
+            }
         }
         LPROF(6);
         lds_sync();
         LPROF(7);
     }
+#pragma unroll
+    for (int i = 0; i < PF; i++) asm volatile("" ::"v"(pf_prev[i]));
 #ifdef TAE_LAT_PROF
     if (blockIdx.x == 0 && lane == 0)
-        printf("latprof wave %2d: dec %llu passA %llu passB %llu bar1 %llu mac %llu bar2 %llu inv %llu bar3 %llu\n", jb,
+        printf("latprof wave %2d: dec %llu bar0 %llu fft %llu bar1 %llu mac %llu bar2 %llu inv %llu bar3 %llu\n", jb,
                (unsigned long long)lprof_[0], (unsigned long long)lprof_[1], (unsigned long long)lprof_[2],
                (unsigned long long)lprof_[3], (unsigned long long)lprof_[4], (unsigned long long)lprof_[5],
                (unsigned long long)lprof_[6], (unsigned long long)lprof_[7]);
@@ -273,7 +300,7 @@ __global__ void __launch_bounds__(THREADS, 1)
 
 inline size_t lds_bytes(int lev) {
     return (size_t)K1 * N * 8 + (size_t)(lev * K1 + K1) * BUF_STRIDE * 16 + 3 * (size_t)M * 16 + 12 * 16 +
-           (size_t)(lev - 1) * K1 * 4 * 64 * 4;
+           (size_t)lev * K1 * M * 4;
 }
 
 }  // namespace br512lat
