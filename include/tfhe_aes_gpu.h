@@ -190,6 +190,27 @@ int tae_aes_encrypt_blocks_raw(const tae_context *ctx, const uint64_t *rk, const
 /* key_schedule on raw fresh key bits [128][L] -> [44*32][L] (either model) */
 int tae_aes_key_schedule_raw(const tae_context *ctx, const uint64_t *key, uint64_t *expanded, int mem);
 
+/* ---- Aes128Encrypt for the fhe_sbox_pbs driver (src/aes_128/fhe/fhe_sbox_pbs.rs:22-171) ------------
+ * ShortintWoppbs1BitSboxPbsAesEncrypt on the 1-bit model (fhe_impls/shortint_woppbs_1bit.rs:47-81:
+ * SubBytes = one 8 -> 8 circuit bootstrap per byte, MixColumns = gf_256_mul by BitCt XORs) and
+ * ShortintWoppbs8BitSboxPbsAesEncrypt on the 8-bit model (same as tae_aes_* there).  On the 1-bit model
+ * every MixColumns breaks the BitCt noise rules, so rounds >= 2 return TAE_E_INDEP before any device work,
+ * where the reference panics "noise components not independent" (its test_light / test_full of this
+ * combination are #[ignore]d, :160-176); rounds == 1 and the key schedule run batched on the device. */
+int tae_aes_sbox_pbs_encrypt_blocks(const tae_context *ctx, const tae_bit *const *expanded_key,
+                                    const tae_bit *const *blocks, size_t n_blocks, int rounds, tae_bit **out);
+/* fhe_sbox_pbs::key_schedule (:123-171): key[128] bits -> expanded[44*32] bits */
+int tae_aes_sbox_pbs_key_schedule(const tae_context *ctx, const tae_bit *const *key, tae_bit **expanded);
+int tae_aes_sbox_pbs_encrypt_blocks_raw(const tae_context *ctx, const uint64_t *rk, const uint64_t *blocks,
+                                        size_t n_blocks, int rounds, uint64_t *out, int mem);
+int tae_aes_sbox_pbs_key_schedule_raw(const tae_context *ctx, const uint64_t *key, uint64_t *expanded, int mem);
+
+/* Static check of a driver's round-function noise schedule for fresh inputs (no context, no device):
+ * TAE_OK, or the status the reference's panic maps to (TAE_E_INDEP / TAE_E_NOISE). */
+#define TAE_DRIVER_GAL_MUL 0  /* fhe_sbox_gal_mul_pbs */
+#define TAE_DRIVER_SBOX_PBS 1 /* fhe_sbox_pbs */
+int tae_aes_noise_schedule_check(int param_set, int driver, int rounds);
+
 /* ---- stage entry points (raw arrays; parity tests and profiling) ---------------------------- */
 int tae_stage_keyswitch(const tae_context *ctx, const uint64_t *in, size_t count, uint64_t *out, int mem);
 int tae_stage_pbs_shift_boolean(const tae_context *ctx, const uint64_t *small, size_t count, int level,

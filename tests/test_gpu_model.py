@@ -180,18 +180,38 @@ def test_readme_counter_mode_batched(keys, golden):
     assert got == [g["ciphertexts"][str(c)] for c in range(1, 11)]
 
 
-def test_sbox_pbs_driver_on_1bit_model_trips_noise_bookkeeping(keys, golden):
-    """ShortintWoppbs1BitSboxPbsAesEncrypt (fhe_impls/shortint_woppbs_1bit.rs:47-81): its reference
-    tests test_light / test_full are #[ignore]d because the leveled MixColumns of fhe_sbox_pbs breaks
-    the BitCt noise rules (:160-176).  The first round's SubBytes + ShiftRows run; MixColumns raises."""
+def test_sbox_pbs_driver_on_1bit_model(keys, golden):
+    """ShortintWoppbs1BitSboxPbsAesEncrypt (fhe_impls/shortint_woppbs_1bit.rs:47-81) on the batched device
+    path.  Its reference tests test_light / test_full are #[ignore]d because the leveled MixColumns of
+    fhe_sbox_pbs breaks the BitCt noise rules (:160-176; tests/test_noise_schedule.py restates why):
+    - key_schedule (fhe_sbox_pbs.rs:123-171): sub_word as batched 8 -> 8 circuit bootstraps, boot_word as
+      128 one-bit identity circuit bootstraps per call, decrypting to the plain AES key schedule;
+    - a 1-round run (ARK, SubBytes of every byte of every block in one call, ShiftRows, ARK) decrypts to
+      the reference's 1-round vectors and equals the GalMul driver's 1-round ciphertexts word for word;
+    - 2 rounds raise NoiseNotIndependent where the reference panics, on both entry points."""
     ck, ctx = keys
+    E = aes_128.ShortintWoppbs1BitSboxPbsAesEncrypt
+    G = aes_128.ShortintWoppbs1BitSboxGalMulPbsAesEncrypt
     g = golden["test_light"]
     key = bytes.fromhex(g["key"])
-    blk = bytes.fromhex(golden["chacha20_zero_seed"]["block1"])
-    ek = aes_128.encrypt_word_array(ck, aes_128.key_schedule_plain(key))
-    block = aes_128.encrypt_byte_array(ck, blk)
-    enc = aes_128.ShortintWoppbs1BitSboxPbsAesEncrypt
-    out = enc.encrypt_block_for_rounds(ctx, ek, block, 1)  # no MixColumns in a 1-round run
-    assert aes_128.decrypt_byte_array(ck, out).hex() == g["block1"]["1"]
-    with pytest.raises((tfhe_aes.NoiseNotIndependent, tfhe_aes.NoiseTooBig)):
-        enc.encrypt_block_for_rounds(ctx, ek, block, 2)
+    ek = E.key_schedule(ctx, aes_128.encrypt_byte_array(ck, key))
+    assert [aes_128.decrypt_byte_array(ck, w) for w in ek] == aes_128.key_schedule_plain(key)
+    assert max(b.noise_level_squared for w in ek[4:] for byte in w for b in byte) == 1  # identity boots
+    blocks = [bytes.fromhex(golden["chacha20_zero_seed"][k]) for k in ("block1", "block2")]
+    enc = [aes_128.encrypt_byte_array(ck, b) for b in blocks]
+    out = E.encrypt_blocks(ctx, ek, enc, 1)
+    assert [aes_128.decrypt_byte_array(ck, o).hex() for o in out] == [g["block1"]["1"], g["block2"]["1"]]
+    assert max(b.noise_level_squared for o in out for byte in o for b in byte) == 9  # SBOX (8) + key bit (1)
+    with pytest.raises(tfhe_aes.NoiseNotIndependent):
+        E.encrypt_block_for_rounds(ctx, ek, enc[0], 2)
+    # raw arrays (fresh inputs): the device key schedule and the 1-round batch
+    kbits = ck.encrypt_bits_raw([b for byte in key for b in aes_128.u8_to_bits(byte)], start_index=600_000)
+    rk = E.key_schedule_raw(ctx, kbits)
+    kb = np.asarray(ck.decrypt_bits_raw(rk)).reshape(176, 8)
+    assert bytes(aes_128.bits_to_u8(x) for x in kb) == b"".join(aes_128.key_schedule_plain(key))
+    cts = ck.encrypt_bits_raw(aes_128.blocks_to_bits(blocks), start_index=700_000).reshape(2, 128, -1)
+    one = E.encrypt_blocks_raw(ctx, rk, cts, rounds=1)
+    assert np.array_equal(one, G.encrypt_blocks_raw(ctx, rk, cts, rounds=1))
+    assert [b.hex() for b in aes_128.bits_to_blocks(ck.decrypt_bits_raw(one))] == [g["block1"]["1"], g["block2"]["1"]]
+    with pytest.raises(tfhe_aes.NoiseNotIndependent):
+        E.encrypt_blocks_raw(ctx, rk, cts, rounds=2)

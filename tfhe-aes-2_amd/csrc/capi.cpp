@@ -572,6 +572,56 @@ int tae_aes_encrypt_blocks_raw(const tae_context *ctx, const uint64_t *rk, const
     });
 }
 
+int tae_aes_sbox_pbs_encrypt_blocks(const tae_context *ctx, const tae_bit *const *expanded_key,
+                                    const tae_bit *const *blocks, size_t n_blocks, int rounds, tae_bit **out) {
+    return guarded([&] {
+        require(ctx && expanded_key && blocks && out, "null");
+        emit(ctx->ctx->aes_encrypt_blocks(unwrap(expanded_key, 44 * 32), unwrap(blocks, 128 * n_blocks), n_blocks,
+                                          rounds, tae::AesDriver::SboxPbs),
+             out);
+    });
+}
+
+int tae_aes_sbox_pbs_key_schedule(const tae_context *ctx, const tae_bit *const *key, tae_bit **expanded) {
+    return guarded([&] {
+        require(ctx && key && expanded, "null");
+        emit(ctx->ctx->aes_key_schedule(unwrap(key, 128), tae::AesDriver::SboxPbs), expanded);
+    });
+}
+
+int tae_aes_sbox_pbs_encrypt_blocks_raw(const tae_context *ctx, const uint64_t *rk, const uint64_t *blocks,
+                                        size_t n_blocks, int rounds, uint64_t *out, int mem) {
+    return guarded([&] {
+        require(ctx && rk && blocks && out, "null");
+        ctx->ctx->aes_encrypt_blocks_raw(rk, blocks, n_blocks, rounds, out, mem == TAE_MEM_DEVICE,
+                                         tae::AesDriver::SboxPbs);
+    });
+}
+
+int tae_aes_sbox_pbs_key_schedule_raw(const tae_context *ctx, const uint64_t *key, uint64_t *expanded, int mem) {
+    return guarded([&] {
+        require(ctx && key && expanded, "null");
+        ctx->ctx->aes_key_schedule_raw(key, expanded, mem == TAE_MEM_DEVICE, tae::AesDriver::SboxPbs);
+    });
+}
+
+int tae_aes_noise_schedule_check(int param_set, int driver, int rounds) {
+    return guarded([&] {
+        const tae::Params p = params_of(param_set);
+        require(driver == TAE_DRIVER_GAL_MUL || driver == TAE_DRIVER_SBOX_PBS, "unknown driver");
+        if (rounds < 1 || rounds > 10) throw tae::ModelError{TAE_E_PARAM, "rounds must be in 1..=10"};
+        std::vector<tae::NoiseLevel> rk(44 * 32), blk(128);
+        for (auto &x : rk) x = p.model == 8 ? tae::NoiseLevel{1, {}} : tae::NoiseLevel::with_noise_level(1, tae::next_ct_id());
+        for (auto &x : blk) x = p.model == 8 ? tae::NoiseLevel{1, {}} : tae::NoiseLevel::with_noise_level(1, tae::next_ct_id());
+        if (p.model == 8)
+            tae::aes8_noise_schedule(rk, blk, rounds, p.max_noise_sq);
+        else if (driver == TAE_DRIVER_SBOX_PBS)
+            tae::sbox_pbs_noise_schedule(rk, blk, rounds, p.max_noise_sq);
+        else
+            tae::aes_noise_schedule(rk, blk, rounds, p.max_noise_sq);
+    });
+}
+
 
 int tae_stage_keyswitch(const tae_context *ctx, const uint64_t *in, size_t count, uint64_t *out, int mem) {
     return guarded([&] {

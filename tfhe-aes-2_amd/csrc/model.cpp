@@ -3,6 +3,7 @@
 #include "model.hpp"
 
 #include <algorithm>
+#include <array>
 #include <cstring>
 
 #include "aes.hpp"
@@ -361,62 +362,125 @@ std::vector<NoiseLevel> aes8_noise_schedule(const std::vector<NoiseLevel> &rk, c
     return st;
 }
 
-void Context::aes_encrypt_blocks_raw(const uint64_t *rk, const uint64_t *blocks, size_t n_blocks, int rounds,
-                                     uint64_t *out, bool device_mem) {
-    if (rounds < 1 || rounds > kAesRounds) throw ModelError{TAE_E_PARAM, "rounds must be in 1..=10"};
+// fhe_sbox_pbs::gf_256_mul (:33-53) on the 1-bit model's noise metadata, XOR by XOR (MSB-first bits,
+// Byte::shl_assign_1 = data_model.rs:45-49).  The loop keeps shifting and reducing the multiplicand
+// after the last multiplier bit: from the fifth iteration on, the leaving bit already carries the
+// component of the original bit 0 that the reduction XORs into bits 3, 4, 6, 7 again, so every call
+// raises "noise components not independent" on non-trivial inputs.
+static std::array<NoiseLevel, 8> gf_256_mul_noise(const std::array<NoiseLevel, 8> &x, uint8_t b, uint64_t max) {
+    std::array<NoiseLevel, 8> a = x, res;  // res = Byte::trivial(ctx, 0)
+    for (int it = 0; it < 8; it++) {
+        if (b & 1)
+            for (int i = 0; i < 8; i++) res[i].add_assign(a[i], max);
+        const NoiseLevel reduce_x8 = a[0];
+        for (int i = 0; i < 7; i++) a[i] = a[i + 1];
+        a[7] = NoiseLevel::trivial();
+        for (int tap : {3, 4, 6, 7}) a[tap].add_assign(reduce_x8, max);
+        b >>= 1;
+    }
+    return res;
+}
+
+// fhe_sbox_pbs::encrypt_block_for_rounds (:75-121) over the 1-bit model (ShortintWoppbs1BitSboxPbsAesEncrypt,
+// fhe_impls/shortint_woppbs_1bit.rs:47-81) on metadata: SubBytes = Byte::sbox_substitute (one 8 -> 8
+// circuit bootstrap, outputs noise^2 = 8 with fresh ids), ShiftRows, MixColumns = the gf_256_mul network
+// (:56-73), AddRoundKey.  MixColumns always raises TAE_E_INDEP (gf_256_mul_noise), which is why the
+// reference #[ignore]s test_light / test_full of this combination (:160-176): only a 1-round run passes.
+std::vector<NoiseLevel> sbox_pbs_noise_schedule(const std::vector<NoiseLevel> &rk, const std::vector<NoiseLevel> &block,
+                                                int rounds, uint64_t max) {
+    auto key_bit = [&](int word, int byte, int bit) -> const NoiseLevel & { return rk[(word * 4 + byte) * 8 + bit]; };
+    std::vector<NoiseLevel> st = block;  // index (4*col + row)*8 + bit (State::from_array)
+    auto xor_state = [&](int w0) {
+        for (int c = 0; c < 4; c++)
+            for (int r = 0; r < 4; r++)
+                for (int b = 0; b < 8; b++) st[(4 * c + r) * 8 + b].add_assign(key_bit(w0 + c, r, b), max);
+    };
+    auto sub_bytes_shift_rows = [&] {
+        std::vector<NoiseLevel> sb(128);
+        for (auto &x : sb) x = NoiseLevel::with_noise_level(8, next_ct_id());
+        for (int c = 0; c < 4; c++)
+            for (int r = 0; r < 4; r++)
+                for (int b = 0; b < 8; b++) st[(4 * c + r) * 8 + b] = sb[(4 * ((c + r) % 4) + r) * 8 + b];
+    };
+    xor_state(0);
+    for (int round = 1; round < rounds; round++) {
+        sub_bytes_shift_rows();
+        std::vector<NoiseLevel> mixed(128);
+        for (int c = 0; c < 4; c++) {
+            std::array<NoiseLevel, 8> col[4];
+            for (int r = 0; r < 4; r++)
+                for (int b = 0; b < 8; b++) col[r][b] = st[(4 * c + r) * 8 + b];
+            for (int i = 0; i < 4; i++) {
+                std::array<NoiseLevel, 8> v = gf_256_mul_noise(col[i], 2, max);
+                for (const auto &[src, m] : {std::pair<int, uint8_t>{(i + 3) % 4, 1}, {(i + 2) % 4, 1}, {(i + 1) % 4, 3}}) {
+                    const std::array<NoiseLevel, 8> t = gf_256_mul_noise(col[src], m, max);
+                    for (int b = 0; b < 8; b++) v[b].add_assign(t[b], max);
+                }
+                for (int b = 0; b < 8; b++) mixed[(4 * c + i) * 8 + b] = v[b];
+            }
+        }
+        st.swap(mixed);
+        xor_state(4 * round);
+    }
+    sub_bytes_shift_rows();
+    xor_state(40);
+    return st;
+}
+
+std::vector<NoiseLevel> Context::block_noise_schedule(AesDriver driver, const std::vector<NoiseLevel> &rk,
+                                                      const std::vector<NoiseLevel> &block, int rounds) const {
+    const uint64_t max = params().max_noise_sq;
+    if (params().model == 8) return aes8_noise_schedule(rk, block, rounds, max);
+    return driver == AesDriver::SboxPbs ? sbox_pbs_noise_schedule(rk, block, rounds, max)
+                                        : aes_noise_schedule(rk, block, rounds, max);
+}
+
+// The device round functions.  1-bit model: Engine::aes_encrypt_blocks (fhe_sbox_gal_mul_pbs rounds, its
+// last round = SubBytes 8 -> 8, ShiftRows, AddRoundKey).  The 1-bit fhe_sbox_pbs driver only gets here
+// with rounds == 1 (its schedule raises at the first MixColumns), where it is exactly that last round.
+void Context::run_aes_blocks(AesDriver driver, const uint64_t *d_rk, const uint64_t *d_in, size_t n_blocks, int rounds,
+                             uint64_t *d_out) {
     if (params().model == 8) {
-        {
-            std::vector<NoiseLevel> krk(44 * 32, NoiseLevel{1, {}}), kbl(128, NoiseLevel{1, {}});
-            aes8_noise_schedule(krk, kbl, rounds, params().max_noise_sq);
-        }
-        const size_t S = bit_len();
-        std::lock_guard<std::mutex> g(mu_);
-        hip_check(hipSetDevice(engine_->device()), "hipSetDevice");
-        if (device_mem) {
-            engine_->order_after_caller();
-            engine_->aes8_encrypt_blocks(rk, blocks, n_blocks, rounds, out);
-            engine_->synchronize();
-            return;
-        }
-        DevBuf d_rk(44 * 32 * S * 8), d_in(n_blocks * 128 * S * 8), d_out(n_blocks * 128 * S * 8);
-        hip_check(hipMemcpyAsync(d_rk.p, rk, 44 * 32 * S * 8, hipMemcpyHostToDevice, engine_->stream()), "upload rk");
-        hip_check(hipMemcpyAsync(d_in.p, blocks, n_blocks * 128 * S * 8, hipMemcpyHostToDevice, engine_->stream()),
-                  "upload blocks");
-        engine_->aes8_encrypt_blocks(d_rk.as<uint64_t>(), d_in.as<uint64_t>(), n_blocks, rounds, d_out.as<uint64_t>());
-        hip_check(hipMemcpyAsync(out, d_out.p, n_blocks * 128 * S * 8, hipMemcpyDeviceToHost, engine_->stream()),
-                  "download");
-        engine_->synchronize();
+        engine_->aes8_encrypt_blocks(d_rk, d_in, n_blocks, rounds, d_out);
         return;
     }
+    if (driver == AesDriver::SboxPbs && rounds != 1)
+        throw ModelError{TAE_E_INDEP, "noise components not independent"};
+    engine_->aes_encrypt_blocks(d_rk, d_in, n_blocks, rounds, d_out);
+}
+
+void Context::aes_encrypt_blocks_raw(const uint64_t *rk, const uint64_t *blocks, size_t n_blocks, int rounds,
+                                     uint64_t *out, bool device_mem, AesDriver driver) {
+    if (rounds < 1 || rounds > kAesRounds) throw ModelError{TAE_E_PARAM, "rounds must be in 1..=10"};
     {
-        // static validation of the fixed AES noise schedule for fresh inputs (noise^2 = 1)
+        // static validation of the fixed noise schedule for fresh inputs (noise^2 = 1, own ids)
         std::vector<NoiseLevel> krk(44 * 32), kbl(128);
-        for (auto &x : krk) x = NoiseLevel::with_noise_level(1, next_ct_id());
-        for (auto &x : kbl) x = NoiseLevel::with_noise_level(1, next_ct_id());
-        aes_noise_schedule(krk, kbl, rounds, params().max_noise_sq);
+        for (auto &x : krk) x = params().model == 8 ? NoiseLevel{1, {}} : NoiseLevel::with_noise_level(1, next_ct_id());
+        for (auto &x : kbl) x = params().model == 8 ? NoiseLevel{1, {}} : NoiseLevel::with_noise_level(1, next_ct_id());
+        block_noise_schedule(driver, krk, kbl, rounds);
     }
+    const size_t S = bit_len();
     std::lock_guard<std::mutex> g(mu_);
     hip_check(hipSetDevice(engine_->device()), "hipSetDevice");
-    const size_t L = params().big_len();
     if (device_mem) {
         engine_->order_after_caller();
-        engine_->aes_encrypt_blocks(rk, blocks, n_blocks, rounds, out);
+        run_aes_blocks(driver, rk, blocks, n_blocks, rounds, out);
         engine_->synchronize();
         return;
     }
-    DevBuf d_rk(44 * 32 * L * 8), d_in(n_blocks * 128 * L * 8), d_out(n_blocks * 128 * L * 8);
-    hip_check(hipMemcpyAsync(d_rk.p, rk, 44 * 32 * L * 8, hipMemcpyHostToDevice, engine_->stream()), "upload rk");
-    hip_check(hipMemcpyAsync(d_in.p, blocks, n_blocks * 128 * L * 8, hipMemcpyHostToDevice, engine_->stream()),
+    DevBuf d_rk(44 * 32 * S * 8), d_in(n_blocks * 128 * S * 8), d_out(n_blocks * 128 * S * 8);
+    hip_check(hipMemcpyAsync(d_rk.p, rk, 44 * 32 * S * 8, hipMemcpyHostToDevice, engine_->stream()), "upload rk");
+    hip_check(hipMemcpyAsync(d_in.p, blocks, n_blocks * 128 * S * 8, hipMemcpyHostToDevice, engine_->stream()),
               "upload blocks");
-    engine_->aes_encrypt_blocks(d_rk.as<uint64_t>(), d_in.as<uint64_t>(), n_blocks, rounds, d_out.as<uint64_t>());
-    hip_check(hipMemcpyAsync(out, d_out.p, n_blocks * 128 * L * 8, hipMemcpyDeviceToHost, engine_->stream()),
+    run_aes_blocks(driver, d_rk.as<uint64_t>(), d_in.as<uint64_t>(), n_blocks, rounds, d_out.as<uint64_t>());
+    hip_check(hipMemcpyAsync(out, d_out.p, n_blocks * 128 * S * 8, hipMemcpyDeviceToHost, engine_->stream()),
               "download");
     engine_->synchronize();
 }
 
 std::vector<BitCt> Context::aes_encrypt_blocks(const std::vector<const BitCt *> &expanded_key,
                                                const std::vector<const BitCt *> &blocks, size_t n_blocks,
-                                               int rounds) {
+                                               int rounds, AesDriver driver) {
     if (expanded_key.size() != 44 * 32) throw ModelError{TAE_E_ARG, "expanded key must be 44 words (1408 bits)"};
     if (blocks.size() != n_blocks * 128) throw ModelError{TAE_E_ARG, "blocks must be 128 bits each"};
     if (rounds < 1 || rounds > kAesRounds) throw ModelError{TAE_E_PARAM, "rounds must be in 1..=10"};
@@ -431,8 +495,7 @@ std::vector<BitCt> Context::aes_encrypt_blocks(const std::vector<const BitCt *> 
     for (size_t blk = 0; blk < n_blocks; blk++) {
         std::vector<NoiseLevel> kb(128);
         for (int i = 0; i < 128; i++) kb[i] = blocks[blk * 128 + i]->noise;
-        out_noise[blk] = params().model == 8 ? aes8_noise_schedule(krk, kb, rounds, params().max_noise_sq)
-                                             : aes_noise_schedule(krk, kb, rounds, params().max_noise_sq);
+        out_noise[blk] = block_noise_schedule(driver, krk, kb, rounds);
     }
     std::vector<uint64_t> rk(44 * 32 * L), in(n_blocks * 128 * L), out(n_blocks * 128 * L);
     for (size_t i = 0; i < 44 * 32; i++) std::memcpy(&rk[i * L], expanded_key[i]->ct.data(), L * 8);
@@ -443,10 +506,7 @@ std::vector<BitCt> Context::aes_encrypt_blocks(const std::vector<const BitCt *> 
         DevBuf d_rk(rk.size() * 8), d_in(in.size() * 8), d_out(out.size() * 8);
         hip_check(hipMemcpyAsync(d_rk.p, rk.data(), rk.size() * 8, hipMemcpyHostToDevice, engine_->stream()), "up");
         hip_check(hipMemcpyAsync(d_in.p, in.data(), in.size() * 8, hipMemcpyHostToDevice, engine_->stream()), "up");
-        if (params().model == 8)
-            engine_->aes8_encrypt_blocks(d_rk.as<uint64_t>(), d_in.as<uint64_t>(), n_blocks, rounds, d_out.as<uint64_t>());
-        else
-            engine_->aes_encrypt_blocks(d_rk.as<uint64_t>(), d_in.as<uint64_t>(), n_blocks, rounds, d_out.as<uint64_t>());
+        run_aes_blocks(driver, d_rk.as<uint64_t>(), d_in.as<uint64_t>(), n_blocks, rounds, d_out.as<uint64_t>());
         hip_check(hipMemcpyAsync(out.data(), d_out.p, out.size() * 8, hipMemcpyDeviceToHost, engine_->stream()), "dn");
         engine_->synchronize();
     }
@@ -462,9 +522,9 @@ std::vector<BitCt> Context::aes_encrypt_blocks(const std::vector<const BitCt *> 
 // fhe_sbox_gal_mul_pbs::key_schedule (:134-164) with ByteT::{sbox_substitute, bootstrap_assign}
 // (fhe_impls/shortint_woppbs_1bit.rs:18-45): words 0..3 = key; word i>=4 from words i-4, i-1
 // (SubWord(RotWord) + Rcon when i%4 == 0), then every bit of word i is bootstrapped (identity LUT).
-std::vector<BitCt> Context::aes_key_schedule(const std::vector<const BitCt *> &key) {
+std::vector<BitCt> Context::aes_key_schedule(const std::vector<const BitCt *> &key, AesDriver driver) {
     if (key.size() != 128) throw ModelError{TAE_E_ARG, "key must be 16 bytes (128 bits)"};
-    if (params().model == 8) return aes8_key_schedule(key);
+    if (params().model == 8 || driver == AesDriver::SboxPbs) return sbox_pbs_key_schedule(key);
     const size_t L = params().big_len();
     std::vector<BitCt> ek(44 * 32);
     for (int i = 0; i < 128; i++) ek[i] = *key[i];
@@ -509,11 +569,16 @@ std::vector<BitCt> Context::aes_key_schedule(const std::vector<const BitCt *> &k
     return ek;
 }
 
-// fhe_sbox_pbs::key_schedule (:123-171) with the 8-bit model's ByteT (fhe_impls/shortint_woppbs_8bit.rs:17-42):
-// sub_word = sbox_substitute of each byte of RotWord(ek[i-1]); after every 4th word the four words
-// i-3..i are boot_word-ed (identity bootstrap_with_lut of each byte).
-std::vector<BitCt> Context::aes8_key_schedule(const std::vector<const BitCt *> &key) {
+// fhe_sbox_pbs::key_schedule (:123-171): sub_word = sbox_substitute of each byte of RotWord(ek[i-1]);
+// after every 4th word the four words i-3..i are boot_word-ed.  ByteT per model:
+//   8-bit (fhe_impls/shortint_woppbs_8bit.rs:17-42): both are Byte::bootstrap_with_lut (SBOX / identity
+//     8 -> 8, outputs NOMINAL);
+//   1-bit (fhe_impls/shortint_woppbs_1bit.rs:17-50): sbox_substitute is one 8 -> 8 circuit bootstrap
+//     (outputs noise^2 = 8), bootstrap_assign one 1 -> 1 identity circuit bootstrap per bit (noise^2 = 1).
+// Every bootstrap of a step goes to the device as one batched call.
+std::vector<BitCt> Context::sbox_pbs_key_schedule(const std::vector<const BitCt *> &key) {
     const size_t L = bit_len();
+    const bool m8 = params().model == 8;
     for (const BitCt *b : key)
         if (b->ct.size() != L) throw ModelError{TAE_E_ARG, "ciphertext size mismatch"};
     std::vector<BitCt> ek(44 * 32);
@@ -524,14 +589,16 @@ std::vector<BitCt> Context::aes8_key_schedule(const std::vector<const BitCt *> &
         ftab_id[x] = (uint64_t)x;
     }
     const Lut sbox = generate_lookup_table(8, 8, ftab_sbox);
-    const Lut ident = generate_lookup_table(8, 8, ftab_id);
-    auto boot = [&](std::vector<BitCt *> bits, const Lut &lut) {  // whole bytes, in place
-        const size_t nbytes = bits.size() / 8;
+    const Lut ident = m8 ? generate_lookup_table(8, 8, ftab_id) : generate_lookup_table(1, 1, ftab_id);
+    auto boot = [&](std::vector<BitCt *> bits, const Lut &lut) {  // groups of lut.input_bits, in place
+        const int n_in = lut.input_bits;
+        const size_t groups = bits.size() / n_in;
         std::vector<uint64_t> in(bits.size() * L), out(bits.size() * L);
         for (size_t t = 0; t < bits.size(); t++) std::memcpy(&in[t * L], bits[t]->ct.data(), L * 8);
-        circuit_bootstrap_raw(in.data(), nbytes, 8, lut, out.data(), false);
+        circuit_bootstrap_raw(in.data(), groups, n_in, lut, out.data(), false);
+        // noise: shortint NOMINAL (8-bit); NOMINAL * input_bit_count (1-bit, shortint_woppbs_1bit.rs:322-325)
         for (size_t t = 0; t < bits.size(); t++)
-            *bits[t] = wrap(std::vector<uint64_t>(out.begin() + t * L, out.begin() + (t + 1) * L), 1);
+            *bits[t] = wrap(std::vector<uint64_t>(out.begin() + t * L, out.begin() + (t + 1) * L), m8 ? 1 : n_in);
     };
     auto bit_at = [&](int word, int byte, int bit) -> BitCt & { return ek[(word * 4 + byte) * 8 + bit]; };
     for (int i = 4; i < 44; i++) {
@@ -564,7 +631,7 @@ std::vector<BitCt> Context::aes8_key_schedule(const std::vector<const BitCt *> &
     return ek;
 }
 
-void Context::aes_key_schedule_raw(const uint64_t *key, uint64_t *expanded, bool device_mem) {
+void Context::aes_key_schedule_raw(const uint64_t *key, uint64_t *expanded, bool device_mem, AesDriver driver) {
     const size_t L = bit_len();
     std::vector<uint64_t> hk(128 * L);
     if (device_mem) {
@@ -579,7 +646,7 @@ void Context::aes_key_schedule_raw(const uint64_t *key, uint64_t *expanded, bool
         kb[i] = wrap(std::vector<uint64_t>(hk.begin() + i * L, hk.begin() + (i + 1) * L), 1);  // fresh
         kp[i] = &kb[i];
     }
-    const std::vector<BitCt> ek = aes_key_schedule(kp);
+    const std::vector<BitCt> ek = aes_key_schedule(kp, driver);
     std::vector<uint64_t> he(44 * 32 * L);
     for (size_t i = 0; i < ek.size(); i++) std::memcpy(&he[i * L], ek[i].ct.data(), L * 8);
     if (device_mem)

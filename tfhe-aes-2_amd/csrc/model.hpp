@@ -8,6 +8,7 @@
 //   src/aes_128/fhe/fhe_impls/shortint_woppbs_1bit.rs:17-151
 //                                            ByteT impls + ShortintWoppbs1BitSboxGalMulPbsAesEncrypt
 //   src/aes_128/fhe/fhe_sbox_gal_mul_pbs.rs:27-191 encrypt_block_for_rounds, key_schedule
+//   src/aes_128/fhe/fhe_sbox_pbs.rs:22-171   the same for the fhe_sbox_pbs driver
 // The ciphertext arithmetic runs in the Engine (HIP); this layer keeps the reference's noise
 // bookkeeping (noise^2 level + independent component ids) on the host, per ciphertext.
 #pragma once
@@ -50,6 +51,8 @@ struct BitCt {
     void xor_assign(const BitCt &rhs);  // BitXorAssign
 };
 
+enum class AesDriver { GalMul, SboxPbs };
+
 struct Lut {  // WopbsLUTBase
     int input_bits = 0, output_bits = 0;
     size_t small_len = 0;
@@ -71,16 +74,21 @@ class Context {  // FheContext
     void circuit_bootstrap_raw(const uint64_t *bits, size_t groups, int n_in, const Lut &lut, uint64_t *out,
                                bool device_mem);
 
-    // Aes128Encrypt::encrypt_block_for_rounds over many blocks (noise bookkeeping per bit)
+    // Aes128Encrypt::encrypt_block_for_rounds over many blocks (noise bookkeeping per bit).  Driver
+    // GalMul = fhe_sbox_gal_mul_pbs (ShortintWoppbs1BitSboxGalMulPbsAesEncrypt); SboxPbs = fhe_sbox_pbs
+    // (ShortintWoppbs1BitSboxPbsAesEncrypt on the 1-bit model).  The 8-bit model has fhe_sbox_pbs only
+    // (ShortintWoppbs8BitSboxPbsAesEncrypt) and ignores the flag.
     std::vector<BitCt> aes_encrypt_blocks(const std::vector<const BitCt *> &expanded_key,
-                                          const std::vector<const BitCt *> &blocks, size_t n_blocks, int rounds);
-    // fhe_sbox_gal_mul_pbs::key_schedule
-    std::vector<BitCt> aes_key_schedule(const std::vector<const BitCt *> &key);
+                                          const std::vector<const BitCt *> &blocks, size_t n_blocks, int rounds,
+                                          AesDriver driver = AesDriver::GalMul);
+    // key_schedule: fhe_sbox_gal_mul_pbs (:134-164) or fhe_sbox_pbs (:123-171)
+    std::vector<BitCt> aes_key_schedule(const std::vector<const BitCt *> &key, AesDriver driver = AesDriver::GalMul);
     // raw arrays, fresh inputs; static noise-schedule validation
     void aes_encrypt_blocks_raw(const uint64_t *rk, const uint64_t *blocks, size_t n_blocks, int rounds,
-                                uint64_t *out, bool device_mem);
-    // raw key schedule (either model): key [128][bit_len] fresh bits -> [44*32][bit_len]
-    void aes_key_schedule_raw(const uint64_t *key, uint64_t *expanded, bool device_mem);
+                                uint64_t *out, bool device_mem, AesDriver driver = AesDriver::GalMul);
+    // raw key schedule: key [128][bit_len] fresh bits -> [44*32][bit_len]
+    void aes_key_schedule_raw(const uint64_t *key, uint64_t *expanded, bool device_mem,
+                              AesDriver driver = AesDriver::GalMul);
 
     // ---- 8-bit model (src/tfhe/shortint_woppbs_8bit.rs, fhe_impls/shortint_woppbs_8bit.rs) ----
     size_t bit_len() const { return params().model == 8 ? params().small_len() : params().big_len(); }
@@ -92,7 +100,11 @@ class Context {  // FheContext
   private:
     template <class F>
     void run8(const uint64_t *in, size_t in_len, uint64_t *out, size_t out_len, bool device_mem, F fn, const Lut *lut);
-    std::vector<BitCt> aes8_key_schedule(const std::vector<const BitCt *> &key);
+    std::vector<BitCt> sbox_pbs_key_schedule(const std::vector<const BitCt *> &key);
+    std::vector<NoiseLevel> block_noise_schedule(AesDriver driver, const std::vector<NoiseLevel> &rk,
+                                                 const std::vector<NoiseLevel> &block, int rounds) const;
+    void run_aes_blocks(AesDriver driver, const uint64_t *d_rk, const uint64_t *d_in, size_t n_blocks, int rounds,
+                        uint64_t *d_out);
     std::unique_ptr<Engine> engine_;
     std::mutex mu_;
 };
@@ -101,6 +113,9 @@ class Context {  // FheContext
 // (per bit) or throws ModelError exactly where the reference would panic.
 std::vector<NoiseLevel> aes_noise_schedule(const std::vector<NoiseLevel> &rk, const std::vector<NoiseLevel> &block,
                                            int rounds, uint64_t max_noise_sq);
+// fhe_sbox_pbs over the 1-bit model: raises TAE_E_INDEP at the first MixColumns (rounds >= 2).
+std::vector<NoiseLevel> sbox_pbs_noise_schedule(const std::vector<NoiseLevel> &rk, const std::vector<NoiseLevel> &block,
+                                                int rounds, uint64_t max_noise_sq);
 // The same for fhe_sbox_pbs with the 8-bit model (additive shortint NoiseLevel, max 11; SubBytes
 // outputs are NOMINAL = 1).
 std::vector<NoiseLevel> aes8_noise_schedule(const std::vector<NoiseLevel> &rk, const std::vector<NoiseLevel> &block,

@@ -33,7 +33,10 @@ EXPORTED = [
     "tae_decrypt_ints_raw", "tae_bootstrap_from_bits_raw", "tae_extract_bits_raw", "tae_aes_key_schedule_raw",
     "tae_last_stage_times_v2", "tae_keys_save", "tae_keys_file_info", "tae_keys_load",
     "tae_last_stage_times_v3", "tae_generate_multivariate_luts", "tae_xor_batch",
+    "tae_aes_sbox_pbs_encrypt_blocks", "tae_aes_sbox_pbs_key_schedule", "tae_aes_sbox_pbs_encrypt_blocks_raw",
+    "tae_aes_sbox_pbs_key_schedule_raw", "tae_aes_noise_schedule_check",
 ]
+TAE_DRIVER_GAL_MUL, TAE_DRIVER_SBOX_PBS = 0, 1
 TAE_KEYS_CLIENT, TAE_KEYS_SERVER = 1, 2
 
 
@@ -107,6 +110,11 @@ def lib() -> C.CDLL:
         "tae_aes_encrypt_blocks": ([vp, vp, vp, sz, C.c_int, vp], C.c_int),
         "tae_aes_key_schedule": ([vp, vp, vp], C.c_int),
         "tae_aes_encrypt_blocks_raw": ([vp, vp, vp, sz, C.c_int, vp, C.c_int], C.c_int),
+        "tae_aes_sbox_pbs_encrypt_blocks": ([vp, vp, vp, sz, C.c_int, vp], C.c_int),
+        "tae_aes_sbox_pbs_key_schedule": ([vp, vp, vp], C.c_int),
+        "tae_aes_sbox_pbs_encrypt_blocks_raw": ([vp, vp, vp, sz, C.c_int, vp, C.c_int], C.c_int),
+        "tae_aes_sbox_pbs_key_schedule_raw": ([vp, vp, vp, C.c_int], C.c_int),
+        "tae_aes_noise_schedule_check": ([C.c_int, C.c_int, C.c_int], C.c_int),
         "tae_stage_keyswitch": ([vp, vp, sz, vp, C.c_int], C.c_int),
         "tae_stage_pbs_shift_boolean": ([vp, vp, sz, C.c_int, vp, C.c_int], C.c_int),
         "tae_stage_bootstrap": ([vp, vp, sz, vp, vp, C.c_int], C.c_int),

@@ -140,72 +140,89 @@ def _flat_bits(x) -> List[BitCt]:
 
 # ---------------------------------------------------------------- Aes128Encrypt ----
 class ShortintWoppbs1BitSboxGalMulPbsAesEncrypt:
-    """fhe_impls/shortint_woppbs_1bit.rs:131-151 -- SBOX + GF x{1,2,3} by one 8->24 WoP-PBS."""
+    """fhe_impls/shortint_woppbs_1bit.rs:131-151 -- SBOX + GF x{1,2,3} by one 8->24 WoP-PBS
+    (fhe_sbox_gal_mul_pbs.rs:84-191).  Every entry point runs batched on the device."""
 
-    @staticmethod
-    def encrypt_block(ctx: FheContext, expanded_key, block):
-        return ShortintWoppbs1BitSboxGalMulPbsAesEncrypt.encrypt_block_for_rounds(ctx, expanded_key, block, ROUNDS)
+    _C = "tae_aes_"  # C-ABI entry points of this driver: <prefix>encrypt_blocks[_raw], <prefix>key_schedule[_raw]
 
-    @staticmethod
-    def encrypt_block_for_rounds(ctx: FheContext, expanded_key, block, rounds: int):
+    @classmethod
+    def _fn(cls, name: str):
+        return getattr(lib(), cls._C + name)
+
+    @classmethod
+    def encrypt_block(cls, ctx: FheContext, expanded_key, block):
+        return cls.encrypt_block_for_rounds(ctx, expanded_key, block, ROUNDS)
+
+    @classmethod
+    def encrypt_block_for_rounds(cls, ctx: FheContext, expanded_key, block, rounds: int):
         """expanded_key: [44][4][8] BitCt (nested or flat); block: [16][8] BitCt -> [16][8]."""
-        ek = _flat_bits(expanded_key)
-        blk = _flat_bits(block)
-        outs = (C.c_void_p * 128)()
-        check(lib().tae_aes_encrypt_block_for_rounds(ctx._h, _handles(ek), _handles(blk), rounds, outs))
-        bits = [BitCt(h, ctx) for h in outs]
-        return [bits[8 * i:8 * i + 8] for i in range(16)]
+        return cls.encrypt_blocks(ctx, expanded_key, [block], rounds)[0]
 
-    @staticmethod
-    def encrypt_blocks(ctx: FheContext, expanded_key, blocks, rounds: int = ROUNDS):
+    @classmethod
+    def encrypt_blocks(cls, ctx: FheContext, expanded_key, blocks, rounds: int = ROUNDS):
         """Batched extension: all blocks' SBOXes of a round go to the GPU as one batch."""
         ek = _flat_bits(expanded_key)
         flat = _flat_bits(blocks)
         nb = len(flat) // 128
         outs = (C.c_void_p * (128 * nb))()
-        check(lib().tae_aes_encrypt_blocks(ctx._h, _handles(ek), _handles(flat), nb, rounds, outs))
+        check(cls._fn("encrypt_blocks")(ctx._h, _handles(ek), _handles(flat), nb, rounds, outs))
         bits = [BitCt(h, ctx) for h in outs]
         return [[bits[b * 128 + 8 * i:b * 128 + 8 * i + 8] for i in range(16)] for b in range(nb)]
 
-    @staticmethod
-    def key_schedule(ctx: FheContext, key):
-        """fhe_sbox_gal_mul_pbs::key_schedule (:134-164): [16][8] BitCt -> [44][4][8]."""
+    @classmethod
+    def key_schedule(cls, ctx: FheContext, key):
+        """key_schedule (fhe_sbox_gal_mul_pbs.rs:134-164 / fhe_sbox_pbs.rs:123-171): [16][8] BitCt -> [44][4][8]."""
         kb = _flat_bits(key)
         outs = (C.c_void_p * (44 * 32))()
-        check(lib().tae_aes_key_schedule(ctx._h, _handles(kb), outs))
+        check(cls._fn("key_schedule")(ctx._h, _handles(kb), outs))
         bits = [BitCt(h, ctx) for h in outs]
         return [[bits[w * 32 + 8 * b:w * 32 + 8 * b + 8] for b in range(4)] for w in range(44)]
 
-    @staticmethod
-    def encrypt_blocks_raw(ctx: FheContext, rk: np.ndarray, blocks: np.ndarray, rounds: int = ROUNDS) -> np.ndarray:
-        """Host arrays: rk [1408][K+1], blocks [n][128][K+1] -> [n][128][K+1]."""
+    @classmethod
+    def encrypt_blocks_raw(cls, ctx: FheContext, rk: np.ndarray, blocks: np.ndarray, rounds: int = ROUNDS) -> np.ndarray:
+        """Host arrays: rk [1408][L], blocks [n][128][L] -> [n][128][L] (L = ctx.lwe_size)."""
         rk = np.ascontiguousarray(rk, dtype=np.uint64)
         blocks = np.ascontiguousarray(blocks, dtype=np.uint64)
         nb = blocks.shape[0]
         out = np.zeros_like(blocks)
-        check(lib().tae_aes_encrypt_blocks_raw(ctx._h, rk.ctypes.data_as(C.c_void_p), blocks.ctypes.data_as(C.c_void_p),
-                                               nb, rounds, out.ctypes.data_as(C.c_void_p), N.TAE_MEM_HOST))
+        check(cls._fn("encrypt_blocks_raw")(ctx._h, rk.ctypes.data_as(C.c_void_p), blocks.ctypes.data_as(C.c_void_p),
+                                            nb, rounds, out.ctypes.data_as(C.c_void_p), N.TAE_MEM_HOST))
         return out
 
-    @staticmethod
-    def encrypt_blocks_device(ctx: FheContext, d_rk: int, d_blocks: int, nb: int, rounds: int, d_out: int):
+    @classmethod
+    def encrypt_blocks_device(cls, ctx: FheContext, d_rk: int, d_blocks: int, nb: int, rounds: int, d_out: int):
         """Device pointers (ints), inputs resident in HBM."""
-        check(lib().tae_aes_encrypt_blocks_raw(ctx._h, C.c_void_p(d_rk), C.c_void_p(d_blocks), nb, rounds,
-                                               C.c_void_p(d_out), N.TAE_MEM_DEVICE))
+        check(cls._fn("encrypt_blocks_raw")(ctx._h, C.c_void_p(d_rk), C.c_void_p(d_blocks), nb, rounds,
+                                            C.c_void_p(d_out), N.TAE_MEM_DEVICE))
 
-
-    @staticmethod
-    def key_schedule_raw(ctx: FheContext, key: np.ndarray) -> np.ndarray:
+    @classmethod
+    def key_schedule_raw(cls, ctx: FheContext, key: np.ndarray) -> np.ndarray:
         """Host arrays: fresh key bits [128][L] -> expanded [1408][L] (L = ctx.lwe_size)."""
         key = np.ascontiguousarray(key, dtype=np.uint64)
         out = np.zeros((44 * 32, ctx.lwe_size), dtype=np.uint64)
-        check(lib().tae_aes_key_schedule_raw(ctx._h, key.ctypes.data_as(C.c_void_p), out.ctypes.data_as(C.c_void_p),
-                                             N.TAE_MEM_HOST))
+        check(cls._fn("key_schedule_raw")(ctx._h, key.ctypes.data_as(C.c_void_p), out.ctypes.data_as(C.c_void_p),
+                                          N.TAE_MEM_HOST))
         return out
 
 
-class ShortintWoppbs8BitSboxPbsAesEncrypt(ShortintWoppbs1BitSboxGalMulPbsAesEncrypt):
-    """fhe_impls/shortint_woppbs_8bit.rs:44-64 -- fhe_sbox_pbs driver over the 8-bit model.
+class ShortintWoppbs1BitSboxPbsAesEncrypt(ShortintWoppbs1BitSboxGalMulPbsAesEncrypt):
+    """fhe_impls/shortint_woppbs_1bit.rs:47-81: the generic fhe_sbox_pbs driver (fhe_sbox_pbs.rs:22-171) over
+    the 1-bit model -- SubBytes = Byte::sbox_substitute (one 8 -> 8 circuit bootstrap per byte, all bytes of
+    all blocks in one batched device call), MixColumns = gf_256_mul by BitCt XORs (:33-73), key_schedule with
+    Byte::bootstrap_assign = one 1 -> 1 identity circuit bootstrap per bit.
+
+    The reference ships this combination with its tests #[ignore]d ("does not work since cipher text noise
+    is not independent in calculations", :160-176): gf_256_mul keeps reducing its multiplicand after the
+    last multiplier bit and XORs a bit into a ciphertext that already holds it, so the first MixColumns
+    raises NoiseNotIndependent (before any device work; tae_aes_noise_schedule_check restates it), exactly
+    where the reference panics.  A 1-round run (no MixColumns) and the key schedule run on the device.
+    """
+
+    _C = "tae_aes_sbox_pbs_"
+
+
+class ShortintWoppbs8BitSboxPbsAesEncrypt(ShortintWoppbs1BitSboxPbsAesEncrypt):
+    """fhe_impls/shortint_woppbs_8bit.rs:44-64 -- the fhe_sbox_pbs driver over the 8-bit model.
 
     Same API; use a context of param set PARAMS_WOPPBS_8BIT (bits are small-key LWEs [n+1]).  SubBytes is
     Byte::bootstrap_with_lut (CBS-VP of the 8 bits into one 8-bit int, then extract_bits), MixColumns is
@@ -213,73 +230,10 @@ class ShortintWoppbs8BitSboxPbsAesEncrypt(ShortintWoppbs1BitSboxGalMulPbsAesEncr
     """
 
 
-class ShortintWoppbs1BitSboxPbsAesEncrypt:
-    """fhe_impls/shortint_woppbs_1bit.rs:47-81: the generic fhe_sbox_pbs driver (fhe_sbox_pbs.rs:22-121)
-    over the 1-bit model -- SubBytes = Byte::sbox_substitute (one 8 -> 8 circuit bootstrap per byte),
-    MixColumns = gf_256_mul by BitCt XORs (:33-73), AddRoundKey / ShiftRows as data_model.rs:270-281.
-
-    The reference ships this combination with its tests #[ignore]d ("does not work since cipher text
-    noise is not independent in calculations", fhe_impls/shortint_woppbs_1bit.rs:160-176): the leveled
-    MixColumns trips the BitCt noise bookkeeping, which raises here exactly as it panics there
-    (NoiseNotIndependent / NoiseTooBig from tae_bit_xor_assign).  Host-driven, one byte per call.
-    """
-
-    @staticmethod
-    def _xor(a: List[BitCt], b: List[BitCt]) -> List[BitCt]:
-        out = [x.clone() for x in a]
-        for x, y in zip(out, b):
-            x ^= y
-        return out
-
-    @staticmethod
-    def _gf_256_mul(ctx: FheContext, a: List[BitCt], b: int) -> List[BitCt]:
-        a = [x.clone() for x in a]
-        res = [ctx.trivial(Cleartext(0)) for _ in range(8)]
-        for _ in range(8):
-            if b & 1:
-                for x, y in zip(res, a):
-                    x ^= y
-            reduce_x8 = a[0]  # Byte::shl_assign_1 (data_model.rs:45-49)
-            a = a[1:] + [ctx.trivial(Cleartext(0))]
-            for i in (3, 4, 6, 7):
-                a[i] ^= reduce_x8
-            b >>= 1
-        return res
-
-    @staticmethod
-    def encrypt_block_for_rounds(ctx: FheContext, expanded_key, block, rounds: int):
-        """expanded_key: [44][4][8] BitCt; block: [16][8] BitCt (byte 4 c + r = state[r][c])."""
-        cls = ShortintWoppbs1BitSboxPbsAesEncrypt
-        lut = ctx.generate_lookup_table(8, 8, lambda v: SBOX[v])
-        state = [[list(block[4 * c + r]) for c in range(4)] for r in range(4)]  # State::from_array
-
-        def xor_state(words):
-            for c in range(4):
-                for r in range(4):
-                    state[r][c] = cls._xor(state[r][c], words[c][r])
-
-        def sub_bytes_shift_rows():
-            for r in range(4):
-                row = [ctx.circuit_bootstrap(state[r][c], lut) for c in range(4)]
-                state[r] = row[r:] + row[:r]
-
-        xor_state(expanded_key[0:4])
-        for i in range(1, rounds):
-            sub_bytes_shift_rows()
-            cols = []
-            for c in range(4):  # mix_columns
-                col = [state[r][c] for r in range(4)]
-                cols.append([cls._xor(cls._xor(cls._xor(cls._gf_256_mul(ctx, col[r], 2),
-                                                        cls._gf_256_mul(ctx, col[(r - 1) % 4], 1)),
-                                               cls._gf_256_mul(ctx, col[(r - 2) % 4], 1)),
-                                      cls._gf_256_mul(ctx, col[(r - 3) % 4], 3)) for r in range(4)])
-            for c in range(4):
-                for r in range(4):
-                    state[r][c] = cols[c][r]
-            xor_state(expanded_key[4 * i:4 * i + 4])
-        sub_bytes_shift_rows()
-        xor_state(expanded_key[40:44])
-        return [state[i % 4][i // 4] for i in range(16)]  # State::into_array
+def noise_schedule_check(param_set: int, driver: int, rounds: int) -> None:
+    """The round function's noise bookkeeping for fresh inputs, without a context or device: raises the
+    error the reference panics with (NoiseNotIndependent / NoiseTooBig), else returns None."""
+    check(lib().tae_aes_noise_schedule_check(param_set, driver, rounds))
 
 
 def counter_blocks(iv: bytes, count: int) -> List[bytes]:
