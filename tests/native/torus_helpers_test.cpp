@@ -23,13 +23,17 @@ static void check_ft(double x) {
     // the kernels' fast path: acc + from_torus(x) whenever it accepts x (and it must accept every
     // |x| in [2^-12, 2^52))
     const uint64_t acc0 = 0x0123456789abcdefull ^ (uint64_t)(int64_t)(x * 7);
-    uint64_t acc = acc0;
-    const bool ok = tae::torus_acc_fast(x, acc);
+    bool ok;
+    const uint64_t acc = tae::torus_add_fast(x, acc0, ok);
     const double ax = std::fabs(x);
     if (ok ? acc != acc0 + b : (ax >= 0x1p-12 && ax < 0x1p52)) {
-        if (fails++ < 10) printf("torus_acc_fast(%a): ok %d got %016llx want %016llx\n", x, (int)ok,
+        if (fails++ < 10) printf("torus_add_fast(%a): ok %d got %016llx want %016llx\n", x, (int)ok,
                                  (unsigned long long)(acc - acc0), (unsigned long long)b);
     }
+    // the kernels' fallback undoes the fast value (linear in acc) and adds the exact one
+    bool d;
+    if (acc - tae::torus_add_fast(x, 0, d) + b != acc0 + b && fails++ < 10)
+        printf("torus_add_fast(%a) is not linear in acc\n", x);
 }
 
 template <int LEV, int B>

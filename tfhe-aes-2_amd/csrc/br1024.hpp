@@ -341,9 +341,15 @@ __global__ void __launch_bounds__(THREADS, 1)
 #pragma unroll
             for (int m = 0; m < 8; m++) {
                 const int j = tt + 64 * m;
-                const cplx r = cmul(v[m], s_utw[j]);
-                poly[j] += from_torus_bits(r.re);
-                poly[j + M] += from_torus_bits(r.im);
+                const cplx t = cmul(v[m], s_utw[j]);
+                bool o0, o1;
+                uint64_t a0 = torus_add_fast(t.re, poly[j], o0), a1 = torus_add_fast(t.im, poly[j + M], o1);
+                if (__builtin_amdgcn_ballot_w64(!(o0 && o1))) {  // zeros, out-of-range magnitudes (rare)
+                    a0 = poly[j] + from_torus_bits(t.re);
+                    a1 = poly[j + M] + from_torus_bits(t.im);
+                }
+                poly[j] = a0;
+                poly[j + M] = a1;
             }
         }
         wave_sync();

@@ -256,9 +256,9 @@ __global__ void __launch_bounds__(THREADS, 1)
             for (int k2 = 0; k2 < 4; k2++) {
                 const int j = ll + 64 * k2;
                 const cplx t = cmul(v[k2], s_utw[j]);
-                uint64_t a0 = poly[j], a1 = poly[j + M];
-                const bool f0 = torus_acc_fast(t.re, a0), f1 = torus_acc_fast(t.im, a1);
-                if (!(f0 && f1)) {  // zeros and out-of-range magnitudes (rare)
+                bool o0, o1;
+                uint64_t a0 = torus_add_fast(t.re, poly[j], o0), a1 = torus_add_fast(t.im, poly[j + M], o1);
+                if (__builtin_amdgcn_ballot_w64(!(o0 && o1))) {  // zeros, out-of-range magnitudes (rare)
                     a0 = poly[j] + from_torus_bits(t.re);
                     a1 = poly[j + M] + from_torus_bits(t.im);
                 }

@@ -12,7 +12,7 @@
 // most every ~14 cycles, four waves keep the SIMD near its ~6-cycle f64 rate): the permlane
 // transposes cost ~7% of the launch and moving them to LDS costs more (+15%, the MAC, table and
 // pass traffic already keeps LDS about half busy); the torus conversion takes the integer fast path
-// (fft_device.hpp torus_acc_fast).
+// (fft_device.hpp torus_add_fast).
 // 16 waves (15 jobs + 1 idle) give the SIMDs four waves each; registers are held under 128 per
 // lane.  The MAC splits the 15 (q, ct) accumulators of a Fourier position 4/4/4/3 over four
 // 256-thread groups (one wave of each group per SIMD).  Lane (u, r) of a job decomposes and
@@ -357,9 +357,9 @@ __global__ void __launch_bounds__(THREADS, 1)
             for (int k2 = 0; k2 < 4; k2++) {
                 const int j = ll + 64 * k2;  // m = r + 4 k2 -> j = u + 16 m
                 const cplx t = cmul(v[k2], s_utw[j]);
-                uint64_t a0 = poly[j], a1 = poly[j + M];
-                const bool f0 = torus_acc_fast(t.re, a0), f1 = torus_acc_fast(t.im, a1);
-                if (!(f0 && f1)) {  // zeros and out-of-range magnitudes (rare; the wave skips it otherwise)
+                bool o0, o1;
+                uint64_t a0 = torus_add_fast(t.re, poly[j], o0), a1 = torus_add_fast(t.im, poly[j + M], o1);
+                if (__builtin_amdgcn_ballot_w64(!(o0 && o1))) {  // zeros, out-of-range magnitudes (rare)
                     a0 = poly[j] + from_torus_bits(t.re);
                     a1 = poly[j + M] + from_torus_bits(t.im);
                 }

@@ -158,24 +158,25 @@ __host__ __device__ __forceinline__ uint64_t from_torus_bits(double x) {
     return r - (uint64_t)((sg != 0) & (r == 0x8000000000000000ull));
 }
 
-// acc + from_torus_bits(x) on the common path, 14 integer VALU ops instead of ~28: when the
-// scaled exponent s = biased exponent - 1011 is in [0, 63] (|x| in [2^-12, 2^52): every inverse-FFT
-// output of the blind rotations except exact zeros), x 2^64 = m 2^s is an integer, the magnitude is
-// m << s (mod 2^64) and the sign is applied as
+// acc + from_torus_bits(x) on the common path, branch-free: when the scaled exponent s = biased
+// exponent - 1011 is in [0, 63] (|x| in [2^-12, 2^52): every inverse-FFT output of the blind rotations
+// except exact zeros), x 2^64 = m 2^s is an integer, the magnitude is m << s (mod 2^64) and the sign is
+// applied as
 //   acc + r = acc + (mag ^ sg) + (neg && mag != 2^63)       (sg = 0 or ~0)
 // i.e. acc - mag for negative x, and acc + 2^63 - 1 for the saturated case mag = 2^63 (x = -(n+1/2)).
-// Returns false (acc untouched) when s is outside [0, 63]; the caller then takes from_torus_bits.
-__host__ __device__ __forceinline__ bool torus_acc_fast(double x, uint64_t &acc) {
+// `ok` is false when s is outside [0, 63] (the returned value is then garbage): the caller takes
+// from_torus_bits for the whole wave behind one wave-uniform branch (12 VALU ops per value here, no exec
+// masking or copies of acc; the per-value branch cost ~17 VALU + 4 SALU).
+__host__ __device__ __forceinline__ uint64_t torus_add_fast(double x, uint64_t acc, bool &ok) {
     const uint64_t b = f64_bits(x);
     const uint32_t hi = (uint32_t)(b >> 32);
     const uint32_t s = ((hi >> 20) & 0x7ff) - 1011u;
-    if (s > 63u) return false;
+    ok = s <= 63u;
     const uint64_t m = (b & 0xFFFFFFFFFFFFFull) | (1ull << 52);
-    const uint64_t mag = m << s;
+    const uint64_t mag = m << (s & 63);
     const uint64_t sg = (uint64_t)(int64_t)((int32_t)hi >> 31);
-    const uint64_t carry = (sg & 1) & (uint64_t)(mag != 0x8000000000000000ull);
-    acc += (mag ^ sg) + carry;
-    return true;
+    const uint64_t carry = (uint64_t)((hi >> 31) & (uint32_t)(mag != 0x8000000000000000ull));
+    return acc + (mag ^ sg) + carry;
 }
 
 // tfhe-rs SignedDecomposer (closest_representable + balanced digits, the carry rule of
