@@ -68,6 +68,32 @@ def test_pfks8_bit_exact(gpu_context8, oracle_keys8, client8):
             assert np.array_equal(out[i, 1, q], oracle_keys8.pfks(q, big[i])), (i, q)
 
 
+@pytest.mark.parametrize("layout", ["k", "rows"])
+def test_pfks8_gemm_layouts_bit_exact(product_raw8, oracle_keys8, layout):
+    """Both PFKS GEMM operand layouts on the 8-bit set (pfks 3 x 2^12: the K layout carries 2 byte limbs
+    per level, 6 slots per coefficient, no offset) over 130 random big LWEs (a ragged second 128-row tile
+    of the row-limb layout) plus digit-range extremes (level digits +-2048, carries, zero, all-ones)."""
+    import os
+    import tfhe_aes
+    os.environ["TAE_PFKS_LAYOUT"] = layout
+    try:
+        ctx = tfhe_aes.context_from_raw(tfhe_aes.PARAMS_WOPPBS_8BIT, product_raw8[1], device=0)
+    finally:
+        del os.environ["TAE_PFKS_LAYOUT"]
+    rng = np.random.default_rng(11)
+    big = rng.integers(0, 2**63, size=(130, 2049), dtype=np.uint64) * np.uint64(2) + rng.integers(
+        0, 2, size=(130, 2049), dtype=np.uint64)
+    ext = np.array([0x8008_0080_0000_0000, 0x7FF8_0080_0000_0000, 0x8007_FF80_0000_0000, 0xFFFF_FFFF_FFFF_FFFF,
+                    0, 0x8000_0000_0000_0000, 0x0008_0000_0000_0000, 0x7FF7_FF7F_F800_0000], dtype=np.uint64)
+    big[3] = np.resize(ext, 2049)
+    out = np.zeros((130, 4, 3, 3 * 1024), dtype=np.uint64)
+    _stage(N.lib().tae_stage_pfks_ggsw, ctx._h, _vp(big), 130, 1, _vp(out), N.TAE_MEM_HOST)
+    for i in (0, 3, 127, 129):
+        for q in (0, 2):
+            assert np.array_equal(out[i, 0, q], oracle_keys8.pfks(q, big[i])), (i, q)
+    del ctx
+
+
 def test_ggsw_fourier8_bit_exact(gpu_context8, oracle_keys8, client8):
     small = client8.encrypt_bits_raw([1], start_index=400)
     ggsw = oracle_keys8.circuit_bootstrap_boolean(small[0])

@@ -111,23 +111,55 @@ def test_pfks_bit_exact(gpu_context, oracle_keys, bits_cts):
             assert np.array_equal(out[i, q], oracle_keys.pfks(q, big[i])), (i, q)
 
 
+# coefficients whose base-2^16 digits hit the ends of their ranges: top digit +32768 / -32767, lower
+# digit +-32768 (with and without the rounding carry), zero and all-ones
+EXTREME = np.array([0x8000_8000_0000_0000, 0x7FFF_8000_0000_0000, 0x8001_7FFF_8000_0000, 0x8000_8000_8000_0000,
+                    0x0000_8000_0000_0000, 0x0000_7FFF_8000_0000, 0xFFFF_8000_0000_0000, 0x7FFF_7FFF_7FFF_FFFF,
+                    0, 0xFFFF_FFFF_FFFF_FFFF, 0x8000_0000_0000_0000, 0x8001_0000_8000_0000], dtype=np.uint64)
+
+
 @pytest.fixture(scope="module")
 def pfks_batch():
-    """150 random big LWEs: one full 128-ciphertext M tile and a ragged one (150 = 128 + 22)."""
+    """400 big LWEs: one full 384-ciphertext M tile of the K-layout GEMM and a ragged one (400 = 384 +
+    16), three full and one ragged 128-ciphertext tiles of the row-limb layout; random coefficients,
+    and rows 5 and 390 made of the digit-range extremes."""
     rng = np.random.default_rng(7)
-    return rng.integers(0, 2**63, size=(150, BIG), dtype=np.uint64) * np.uint64(2) + rng.integers(
-        0, 2, size=(150, BIG), dtype=np.uint64)
+    big = rng.integers(0, 2**63, size=(400, BIG), dtype=np.uint64) * np.uint64(2) + rng.integers(
+        0, 2, size=(400, BIG), dtype=np.uint64)
+    for row in (5, 390):
+        big[row] = np.resize(EXTREME, BIG)
+    return big
 
 
-def test_pfks_gemm_ragged_bit_exact(gpu_context, oracle_keys, pfks_batch):
-    """The PFKS GEMM (ksgemm::gemm_g6, 384-row tiles = 128 ciphertexts x 3 digit limbs) on a ragged
-    batch of 150 random inputs: a full and a partial M tile; rows from both equal the oracle's private
-    functional keyswitch (the scalar u64 kernel, used by params_sqrd_lvl_1, is pinned through
-    test_gpu_model8.py::test_other_n1024_sets_bit_exact)."""
+def _layout_context(product_raw, layout):
+    """A context whose PFKS GEMM is forced to one operand layout (TAE_PFKS_LAYOUT, read at creation;
+    the product picks the K layout from 2048 ciphertexts on)."""
+    import os
+    import tfhe_aes
+    os.environ["TAE_PFKS_LAYOUT"] = layout
+    try:
+        return tfhe_aes.context_from_raw(tfhe_aes.PARAMS_SQRD_LVL_64, product_raw[1], device=0)
+    finally:
+        del os.environ["TAE_PFKS_LAYOUT"]
+
+
+@pytest.fixture(scope="module")
+def layout_contexts(product_raw):
+    return {lay: _layout_context(product_raw, lay) for lay in ("k", "rows")}
+
+
+@pytest.mark.parametrize("layout", ["k", "rows"])
+def test_pfks_gemm_ragged_bit_exact(layout_contexts, oracle_keys, pfks_batch, layout):
+    """The PFKS GEMM (ksgemm::gemm_g6) in both operand layouts -- K layout (5 limb slots per
+    coefficient, 384-ciphertext tiles, digit-offset correction) and 6-bit row-tile limbs (384-row tiles
+    = 128 ciphertexts x 3 limbs) -- on a ragged batch: rows from full and partial M tiles, including
+    the digit-range extremes, equal the oracle's private functional keyswitch (the scalar u64 kernel,
+    used by params_sqrd_lvl_1, is pinned through test_gpu_model8.py::test_other_n1024_sets_bit_exact)."""
+    ctx = layout_contexts[layout]
     big = pfks_batch
     out = np.zeros((len(big), 5, 5 * 512), dtype=np.uint64)
-    _stage(N.lib().tae_stage_pfks_ggsw, gpu_context._h, _vp(big), len(big), 1, _vp(out), N.TAE_MEM_HOST)
-    for i in (0, 63, 127, 128, 149):
+    _stage(N.lib().tae_stage_pfks_ggsw, ctx._h, _vp(big), len(big), 1, _vp(out), N.TAE_MEM_HOST)
+    for i in (0, 5, 127, 128, 383, 384, 390, 399):
         for q in (0, 4):
             assert np.array_equal(out[i, q], oracle_keys.pfks(q, big[i])), (i, q)
 

@@ -15,6 +15,7 @@
 
 #include "client.hpp"
 #include "cplx.hpp"
+#include "kslots.hpp"
 #include "params.hpp"
 
 namespace tae {
@@ -158,6 +159,15 @@ class Engine {
     void collect_times();
     // int8 MFMA keyswitches (ksgemm.hpp): key limb matrices + digit scratch
     bool mfma_ks_ = false;
+    // PFKS GEMM in the K layout (ksgemm.hpp KSlots) from pf_kl_min_ ciphertexts on, the 6-bit
+    // row-tile limbs below (shorter K: 2.4x fewer K steps per tile, for batches too small to fill the
+    // chip either way); TAE_PFKS_LAYOUT=k / rows forces one (the parity tests run both)
+    bool pf_kl_ = false;
+    long pf_kl_min_ = 2048;
+    int kp_pf_kl_ = 0;
+    ksgemm::KSlots pf_slots_;
+    int8_t *d_pf_bt_kl_ = nullptr;
+    uint64_t *d_pf_corr_ = nullptr;  // [ncols] digit-offset correction of the K layout
     int8_t *d_pf_bt_ = nullptr, *d_ks_bt_ = nullptr, *d_digits_ = nullptr;
     size_t cap_digits_ = 0;
     int kp_pf_ = 0, kp_ks_ = 0;

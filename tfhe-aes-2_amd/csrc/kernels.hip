@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <climits>
 #include <cstring>
 #include <stdexcept>
 
@@ -683,6 +684,8 @@ Engine::Engine(const ServerKeyRaw &keys, int device) : p_(keys.p), device_(devic
 void Engine::prepare_mfma_keys() {
     HIPC(hipFuncSetAttribute((const void *)ksgemm::gemm_g6<6, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)ksgemm::gemm_g6_lds<4>()));
+    HIPC(hipFuncSetAttribute((const void *)ksgemm::gemm_g6<6, 4, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)ksgemm::gemm_g6_lds<4>()));
     // int8-MFMA keyswitches when the digits fit their limbs (PFKS 17-bit digits as 3 x 6-bit limbs,
     // KS digits as one byte); otherwise (params_sqrd_lvl_1: pfks base 2^24) the u64 VALU kernels
     mfma_ks_ = p_.pfks_b <= 16 && p_.ks_b <= 7;
@@ -692,12 +695,27 @@ void Engine::prepare_mfma_keys() {
     kp_pf_ = (kd_pf + ksgemm::TK - 1) / ksgemm::TK * ksgemm::TK;
     kp_ks_ = (kd_ks + ksgemm::TK - 1) / ksgemm::TK * ksgemm::TK;
     const int nc_pf = (p_.k + 1) * glwe, nc_ks = p_.n + 1;
+    const long pf_blk = (long)(p_.K() + 1) * p_.pfks_l * glwe;
     d_pf_bt_ = static_cast<int8_t *>(alloc((size_t)nc_pf * 8 * kp_pf_));
     d_ks_bt_ = static_cast<int8_t *>(alloc((size_t)nc_ks * 8 * kp_ks_));
     dim3 gpf((kp_pf_ + 63) / 64, (nc_pf + 63) / 64), gks((kp_ks_ + 63) / 64, (nc_ks + 63) / 64);
     // the LDS-DMA GEMM reads both operands row-pair interleaved (ksgemm::op_off; Kp % 128 == 0)
-    ksgemm::prep_key<<<gpf, kThreads, 0, stream_>>>(d_pfpksk_, d_pf_bt_, kd_pf, kp_pf_, nc_pf, glwe, glwe,
-                                                    (long)(p_.K() + 1) * p_.pfks_l * glwe, true);
+    ksgemm::prep_key<<<gpf, kThreads, 0, stream_>>>(d_pfpksk_, d_pf_bt_, kd_pf, kp_pf_, nc_pf, glwe, glwe, pf_blk, true);
+    pf_kl_ = ksgemm::kslots_build(p_.pfks_b, p_.pfks_l, pf_slots_);
+    if (const char *lay = getenv("TAE_PFKS_LAYOUT")) {
+        if (!strcmp(lay, "rows")) pf_kl_min_ = LONG_MAX;
+        if (!strcmp(lay, "k")) pf_kl_min_ = 0;
+    }
+    if (pf_kl_) {  // K-layout key rows (limbs in K) and the per-column offset correction
+        kp_pf_kl_ = ((p_.K() + 1) * pf_slots_.S + ksgemm::TK - 1) / ksgemm::TK * ksgemm::TK;
+        d_pf_bt_kl_ = static_cast<int8_t *>(alloc((size_t)nc_pf * 8 * kp_pf_kl_));
+        dim3 gkl((kp_pf_kl_ + 63) / 64, (nc_pf + 63) / 64);
+        ksgemm::prep_key_kl<<<gkl, kThreads, 0, stream_>>>(d_pfpksk_, d_pf_bt_kl_, p_.K() + 1, p_.pfks_l, kp_pf_kl_,
+                                                           nc_pf, glwe, glwe, pf_blk, pf_slots_);
+        d_pf_corr_ = static_cast<uint64_t *>(alloc((size_t)nc_pf * 8));
+        ksgemm::key_offset_corr<<<(nc_pf + 255) / 256, 256, 0, stream_>>>(d_pfpksk_, d_pf_corr_, p_.K() + 1, p_.pfks_l,
+                                                                          nc_pf, glwe, glwe, pf_blk, pf_slots_);
+    }
     ksgemm::prep_key<<<gks, kThreads, 0, stream_>>>(d_ksk_, d_ks_bt_, kd_ks, kp_ks_, nc_ks, nc_ks, nc_ks, 0);
     HIPC(hipGetLastError());
     HIPC(hipStreamSynchronize(stream_));
@@ -739,7 +757,7 @@ Engine::~Engine() {
     }
     for (void *q : {(void *)d_bsk_f_, (void *)d_twist_, (void *)d_untwist_, (void *)d_w_, (void *)d_lut_shift_,
                     (void *)d_lut24_, (void *)d_lut8_, (void *)d_small_, (void *)d_big_, (void *)d_ggsw_,
-                    (void *)d_ggsw_f_, (void *)d_state_, (void *)d_muls_, (void *)d_pf_bt_, (void *)d_ks_bt_,
+                    (void *)d_ggsw_f_, (void *)d_state_, (void *)d_muls_, (void *)d_pf_bt_, (void *)d_ks_bt_, (void *)d_pf_corr_, (void *)d_pf_bt_kl_,
                     (void *)d_digits_, (void *)d_wlut_sbox_, (void *)d_wlut_id_, (void *)d_lut_x_, (void *)d_xbuf_,
                     (void *)d_xsh_, (void *)d_xks_, (void *)d_xpbs_, (void *)d_ints_})
         if (q) hipFree(q);
@@ -842,6 +860,23 @@ void Engine::pbs_shift_boolean(const uint64_t *d_small, uint64_t *d_big, size_t 
 void Engine::pfks_into_ggsw(const uint64_t *d_big, uint64_t *d_ggsw, size_t B, int level) {
     if (!B) return;
     const int glwe = (int)p_.glwe_len();
+    if (mfma_ks_ && pf_kl_ && (long)B >= pf_kl_min_) {
+        // K layout: rows = ciphertexts, K = (K+1) x S limb slots (ksgemm.hpp KSlots)
+        const int K = p_.K(), kd = (K + 1) * pf_slots_.S;
+        const long mt = (long)((B + 383) / 384);  // 384-ciphertext tiles
+        ensure_digits(d_digits_, cap_digits_, (size_t)mt * 384, kd, kp_pf_kl_, stream_, true);
+        const size_t thr = B * (size_t)(K + 1);
+        ksgemm::prep_digits_kl<<<(unsigned)((thr + 255) / 256), 256, 0, stream_>>>(
+            d_big, K + 1, d_digits_, (long)B, K + 1, kp_pf_kl_, p_.pfks_b, p_.pfks_l, pf_slots_);
+        const int ncols = (p_.k + 1) * glwe;
+        const long out_stride = (long)p_.cbs_l * ncols;
+        const long ntiles = ((long)ncols * 8 + ksgemm::BTN - 1) / ksgemm::BTN;
+        uint64_t *dst = d_ggsw + (size_t)(level - 1) * ncols;
+        ksgemm::gemm_g6<6, 4, true><<<(unsigned)(mt * ntiles), 1024, ksgemm::gemm_g6_lds<4>(), stream_>>>(
+            d_digits_, d_pf_bt_kl_, kp_pf_kl_, mt, ncols, dst, out_stride, (long)B, d_pf_corr_);
+        HIPC(hipGetLastError());
+        return;
+    }
     if (mfma_ks_) {
         // digits as 3 balanced 6-bit limbs, limb index in the MFMA row tile (ksgemm.hpp gemm_g6)
         const int K = p_.K(), kd = (K + 1) * p_.pfks_l;

@@ -24,6 +24,8 @@
 
 #include <cstdint>
 
+#include "kslots.hpp"
+
 namespace tae {
 namespace ksgemm {
 
@@ -285,6 +287,100 @@ __global__ void __launch_bounds__(256) prep_digits3(const uint64_t *__restrict__
     }
 }
 
+// ---- PFKS in the K layout: the digit limbs go into the K dimension instead of the row tile ----
+// Slot s of big-LWE coefficient i (K index i * S + s) holds limb limb(s) of the level-lev(s) digit,
+// and the key rows are pre-shifted to match:
+//   A[b][i S + s]       = limb_{limb(s)}(d_{lev(s)}[b][i] - c_{lev(s)})      (balanced signed bytes)
+//   B[(col, j)][i S + s] = byte j of (KEY[i][lev(s)][col] << 8 limb(s))
+// so sum_s A B recombines as sum_j 256^j P[b][(col, j)] = sum_{i,l} (d_l - c_l) KEY[i][l][col]
+// (mod 2^64), and the offsets come back through corr[col] = sum_{i,l} c_l KEY[i][l][col].  Each level
+// gets the fewest 8-bit limbs that hold its digit range after an offset: params_sqrd_lvl_64 (base
+// 2^16, 2 levels) has the top digit in [-32767, 32768] (2 limbs with c = 129: [-32896, 32639] + 129)
+// and the lower one in [-32768, 32768] (3 limbs) -- 5 slots per coefficient against 2 x 3 rows of the
+// 6-bit row-tile layout, 17% fewer MFMAs; base 2^12 (8-bit model, lvl_256) needs 2 limbs per level
+// instead of 3.  i32 sums stay exact: 128 * 128 * S (K+1) < 2^31 for every set here.
+// digits in the K layout, row-pair interleaved rows b (op_off): one thread per (b, i)
+__global__ void __launch_bounds__(256) prep_digits_kl(const uint64_t *__restrict__ in, long in_stride,
+                                                      int8_t *__restrict__ A, long B, int n_in, int Kp, int base_log,
+                                                      int levels, KSlots ks) {
+    const long t = (long)blockIdx.x * 256 + threadIdx.x;
+    const long b = t / n_in;
+    const int i = (int)(t - b * n_in);
+    if (b >= B) return;
+    const uint64_t x = in[b * in_stride + i];
+    const int nrb = 64 - base_log * levels;
+    uint64_t s = x >> (nrb - 1);
+    s += s & 1;
+    s >>= 1;
+    const uint64_t mask = (1ull << base_log) - 1;
+    for (int lev = levels; lev >= 1; lev--) {
+        const uint64_t res = s & mask;
+        s >>= base_log;
+        uint64_t carry = ((res - 1) | s) & res;
+        carry >>= (base_log - 1);
+        s += carry;
+        int64_t d = (int64_t)(res - (carry << base_log)) - ks.off[lev - 1];
+        const int n = ks.nlimb[lev - 1];
+        const long k0 = (long)i * ks.S + ks.first[lev - 1];
+        for (int m = 0; m < n; m++) {
+            int64_t limb;
+            if (m == n - 1) {
+                limb = d;
+            } else {
+                limb = ((d + 128) & 255) - 128;
+                d = (d - limb) >> 8;
+            }
+            A[op_off(b, k0 + m, Kp, true)] = (int8_t)limb;
+        }
+    }
+}
+
+// key rows in the K layout (prep_key with the slot shift): element (kd = i * L + l, col) of the u64
+// key at key[kd * key_kd_stride + (col / cols_per_block) * key_blk_stride + col % cols_per_block]
+__global__ void __launch_bounds__(256) prep_key_kl(const uint64_t *__restrict__ key, int8_t *__restrict__ Bt, int n_coef,
+                                                   int levels, int Kp, int ncols, int cols_per_block, long key_kd_stride,
+                                                   long key_blk_stride, KSlots ks) {
+    __shared__ int8_t tile[64][8][65];
+    const int k0 = blockIdx.x * 64, col0 = blockIdx.y * 64;
+    for (int t = threadIdx.x; t < 64 * 64; t += 256) {
+        const int kk = t >> 6, cc = t & 63;
+        const int k = k0 + kk, col = col0 + cc;
+        int8_t lb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        const int i = k / ks.S, sl = k - i * ks.S;
+        if (i < n_coef && col < ncols) {
+            const long kd = (long)i * levels + ks.lev[sl];
+            const uint64_t v = key[kd * key_kd_stride + (long)(col / cols_per_block) * key_blk_stride + col % cols_per_block];
+            key_limbs(v << (8 * ks.limb[sl]), lb);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) tile[cc][j][kk] = lb[j];
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < 64 * 8 * 64; t += 256) {
+        const int kk = t & 63, row = t >> 6;
+        const int cc = row >> 3, j = row & 7;
+        const int col = col0 + cc, k = k0 + kk;
+        if (col < ncols && k < Kp) Bt[op_off((long)col * 8 + j, k, Kp, true)] = tile[cc][j][kk];
+    }
+}
+
+// corr[col] = sum_{i, l} c_l KEY[i][l][col] (mod 2^64)
+__global__ void __launch_bounds__(256) key_offset_corr(const uint64_t *__restrict__ key, uint64_t *__restrict__ corr,
+                                                       int n_coef, int levels, int ncols, int cols_per_block,
+                                                       long key_kd_stride, long key_blk_stride, KSlots ks) {
+    const int col = blockIdx.x * 256 + threadIdx.x;
+    if (col >= ncols) return;
+    const uint64_t *kc = key + (long)(col / cols_per_block) * key_blk_stride + col % cols_per_block;
+    uint64_t acc = 0;
+    for (int l = 0; l < levels; l++) {
+        if (!ks.off[l]) continue;
+        uint64_t sum = 0;
+        for (int i = 0; i < n_coef; i++) sum += kc[((long)i * levels + l) * key_kd_stride];
+        acc += (uint64_t)ks.off[l] * sum;
+    }
+    corr[col] = acc;
+}
+
 // ---- gemm_g6: the PFKS GEMM (3-limb digits, LDS-DMA staging) ----
 // - Staging: global_load_lds (16 B per lane, no VGPR staging, no ds_write) into a ring of G4S stages
 //   of 64-byte K steps; two steps stay in flight across the per-step barrier by a counted vmcnt
@@ -321,10 +417,12 @@ __device__ __forceinline__ void g4_glds(const int8_t *src, int8_t *lds_base) {
 template <int WM>
 inline size_t gemm_g6_lds() { return (size_t)G4S * (96 * WM + BTN) * G4K; }
 
-template <int LB3, int WM>
+// KL: K-layout operands (prep_digits_kl / prep_key_kl): tile rows are ciphertexts, the epilogue only
+// recombines the 8 key limbs and adds corr[col].
+template <int LB3, int WM, bool KL = false>
 __global__ void __launch_bounds__(256 * WM, 1)
     gemm_g6(const int8_t *__restrict__ A, const int8_t *__restrict__ Bt, int Kp, long mtiles, int ncols,
-            uint64_t *__restrict__ out, long out_stride, long B) {
+            uint64_t *__restrict__ out, long out_stride, long B, const uint64_t *__restrict__ corr = nullptr) {
     constexpr int TMR = 96 * WM, NW = 4 * WM;              // tile rows, waves
     constexpr int SA = TMR * G4K, SAB = (TMR + BTN) * G4K;  // stage bytes
     constexpr int NPA = TMR / 16, NP = NPA + BTN / 16;      // 16-row pieces per stage
@@ -426,6 +524,41 @@ __global__ void __launch_bounds__(256 * WM, 1)
     }
 
     const int j = r & 7;
+    if constexpr (KL) {
+        // The 8 key-limb sums of an output sit in 8 lanes; instead of shuffling, each m-tile goes
+        // through this wave's part of the (now idle) staging ring: E[row][tj 32 + r] (rows padded to 68
+        // dwords: the 16 lanes of a ds_read_b128 group read 16 rows on distinct banks), then every lane
+        // reads whole outputs' limbs (2 x b128) and stores them -- no spills, all lanes storing.
+        static_assert(16 * 32 * 68 * 4 * WM / 4 <= G4S * (96 * WM + BTN) * G4K, "epilogue fits the ring");
+        __syncthreads();  // every wave is done with the ring
+        int *E = reinterpret_cast<int *>(smem_g) + wave * 32 * 68;
+        const long b0 = row0 + wm * 96;
+        const long colb = (col8_0 + wn * 64) >> 3;  // first key column of this wave
+#pragma unroll
+        for (int m = 0; m < 3; m++) {
+#pragma unroll
+            for (int tj = 0; tj < 2; tj++)
+#pragma unroll
+                for (int q = 0; q < 16; q++) E[((q & 3) + 8 * (q >> 2) + 4 * h) * 68 + tj * 32 + r] = acc[m][tj][q];
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local hand-off
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int row = lane & 31, g = (lane >> 5) + 2 * k;  // g: 8-column group = key column
+                const v4i lo = *reinterpret_cast<const v4i *>(E + row * 68 + 8 * g);
+                const v4i hi = *reinterpret_cast<const v4i *>(E + row * 68 + 8 * g + 4);
+                uint64_t v = 0;
+#pragma unroll
+                for (int jj = 0; jj < 4; jj++) {
+                    v += (uint64_t)(int64_t)lo[jj] << (8 * jj);
+                    v += (uint64_t)(int64_t)hi[jj] << (8 * (jj + 4));
+                }
+                const long b = b0 + 32 * m + row, col = colb + g;
+                if (col < ncols && b < B) out[b * out_stride + col] = 0 - (v + corr[col]);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next m overwrites
+        }
+        return;
+    }
     const long b0 = (mt * WM + wm) * 32;
 #pragma unroll
     for (int tj = 0; tj < 2; tj++) {
