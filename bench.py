@@ -81,12 +81,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = local
+    # one rank per GPU; TAE_BENCH_BACKEND=gloo rehearses the multi-rank path with several ranks on one
+    # GPU (RCCL refuses two ranks on one device): same key broadcast, device-key contexts and timing
+    backend = os.environ.get("TAE_BENCH_BACKEND", "nccl")
+    dev = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     torch.cuda.set_device(dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
     threads = min(16, os.cpu_count() or 1)
     pid = tfhe_aes.PARAMS_SQRD_LVL_64 if args.model == "1bit" else tfhe_aes.PARAMS_WOPPBS_8BIT
     p = tfhe_aes.get_params(pid)
