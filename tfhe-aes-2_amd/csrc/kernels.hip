@@ -282,6 +282,15 @@ __global__ void __launch_bounds__(kThreads) cmux_tree_kernel(const cplx *__restr
 // Forward torus FFT of many polynomials (GGSW / BSK to the Fourier domain).  TPJ threads per
 // polynomial, 256/TPJ polynomials per workgroup.
 // ---------------------------------------------------------------------------------------------
+// N = 512 (R = 16, 16 threads per polynomial): the spectrum sits in LDS with one pad slot per 16
+// (fft_pidx) and a polynomial stride of 273 slots, so pass 1's stride-16 column reads and the four
+// polynomials of a wave fall on different banks (unpadded: 16-way conflicts, 5.5 conflict cycles per
+// LDS instruction in the round-1 PMC).
+template <int M>
+__device__ __forceinline__ int fft_pidx(int f) { return M == 256 ? f + (f >> 4) : f; }
+template <int M>
+constexpr int fft_poly_stride() { return M == 256 ? 273 : M; }
+
 template <int N>
 __global__ void __launch_bounds__(kThreads) fft_torus_kernel(const uint64_t *__restrict__ in, cplx *__restrict__ out,
                                                           size_t count, const cplx *__restrict__ twist,
@@ -293,7 +302,7 @@ __global__ void __launch_bounds__(kThreads) fft_torus_kernel(const uint64_t *__r
     const int local = threadIdx.x / TPJ, u = threadIdx.x - local * TPJ;
     const size_t poly = (size_t)blockIdx.x * JPB + local;
     const bool active = poly < count;
-    cplx *X = buf + local * M;
+    cplx *X = buf + local * fft_poly_stride<M>();
     if (active) {
         const uint64_t *src = in + poly * N;
         cplx v[R];
@@ -306,7 +315,7 @@ __global__ void __launch_bounds__(kThreads) fft_torus_kernel(const uint64_t *__r
         }
         dft<R, M, false>(v, w);
 #pragma unroll
-        for (int kk = 0; kk < R; kk++) X[u + kk * TPJ] = (u * kk) ? cmul(v[kk], w[u * kk]) : v[kk];
+        for (int kk = 0; kk < R; kk++) X[fft_pidx<M>(u + kk * TPJ)] = (u * kk) ? cmul(v[kk], w[u * kk]) : v[kk];
     }
     __syncthreads();
     int L = TPJ / R;
@@ -314,20 +323,21 @@ __global__ void __launch_bounds__(kThreads) fft_torus_kernel(const uint64_t *__r
     for (int s = 1; s < P; s++, L /= R) {
         if (active) {
             const int gg = u / L, uu = u - gg * L;
-            cplx *base = X + gg * R * L + uu;
+            const int b0 = gg * R * L + uu;
             cplx v[R];
 #pragma unroll
-            for (int m = 0; m < R; m++) v[m] = base[m * L];
+            for (int m = 0; m < R; m++) v[m] = X[fft_pidx<M>(b0 + m * L)];
             dft<R, M, false>(v, w);
             const int step = M / (R * L);
 #pragma unroll
-            for (int kk = 0; kk < R; kk++) base[kk * L] = (uu * kk) ? cmul(v[kk], w[uu * kk * step]) : v[kk];
+            for (int kk = 0; kk < R; kk++)
+                X[fft_pidx<M>(b0 + kk * L)] = (uu * kk) ? cmul(v[kk], w[uu * kk * step]) : v[kk];
         }
         __syncthreads();
     }
     if (active) {
         cplx *dst = out + poly * M;
-        for (int f = u; f < M; f += TPJ) dst[f] = X[f];
+        for (int f = u; f < M; f += TPJ) dst[f] = X[fft_pidx<M>(f)];
     }
 }
 
@@ -655,7 +665,7 @@ void Engine::bsk_to_fourier(const uint64_t *d_bsk_std) {
     const int M = p_.M();
     if (p_.N == 512) {
         constexpr int JPB = kThreads / (256 / 16);
-        fft_torus_kernel<512><<<(unsigned)((polys + JPB - 1) / JPB), kThreads, JPB * M * sizeof(cplx), stream_>>>(
+        fft_torus_kernel<512><<<(unsigned)((polys + JPB - 1) / JPB), kThreads, JPB * fft_poly_stride<256>() * sizeof(cplx), stream_>>>(
             d_bsk_std, d_bsk_f_, polys, d_twist_, d_w_);
     } else {
         constexpr int JPB = kThreads / (512 / 8);
@@ -906,7 +916,7 @@ void Engine::ggsw_to_fourier(const uint64_t *d_ggsw, cplx *d_ggsw_f, size_t B) {
     const int M = p_.M();
     if (p_.N == 512) {
         constexpr int JPB = kThreads / 16;
-        fft_torus_kernel<512><<<(unsigned)((polys + JPB - 1) / JPB), kThreads, JPB * M * sizeof(cplx), stream_>>>(
+        fft_torus_kernel<512><<<(unsigned)((polys + JPB - 1) / JPB), kThreads, JPB * fft_poly_stride<256>() * sizeof(cplx), stream_>>>(
             d_ggsw, d_ggsw_f, polys, d_twist_, d_w_);
     } else {
         constexpr int JPB = kThreads / 64;
