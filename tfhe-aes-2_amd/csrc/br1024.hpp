@@ -92,6 +92,10 @@ __global__ void __launch_bounds__(THREADS, 1)
     cplx *s_tw = buf + JOBS * BUF_STRIDE;                           // twist
     cplx *s_w = s_tw + M;                                           // W_512 table
     cplx *s_utw = s_w + M;                                          // untwist = conj(twist) / M
+    // per-lane twiddles of passes 0 and 1 in lane order: s_w[t k] / s_w[8 (t & 7) k] read straight from
+    // the W table put 2-8 lanes of a b128 group on one bank (PMC: conflict cycles ~ all LDS cycles)
+    cplx *s_w0 = s_utw + M;                                         // [k - 1][t] = W_512^{t k}, k = 1..7
+    cplx *s_w1 = s_w0 + 7 * 64;                                     // [k - 1][uu] = W_512^{8 uu k}
     const int tid = threadIdx.x;
     const int jb = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int t = tid & 63;
@@ -117,6 +121,8 @@ __global__ void __launch_bounds__(THREADS, 1)
         s_w[i] = wtab[i];
         s_utw[i] = untwist[i];
     }
+    for (int i = tid; i < 7 * 64; i += THREADS) s_w0[i] = wtab[(i & 63) * ((i >> 6) + 1)];
+    if (tid < 7 * 8) s_w1[tid] = wtab[8 * (tid & 7) * ((tid >> 3) + 1)];
     const cplx *gbase = PBS ? ggsw_base : ggsw_base + (size_t)g * n_in * ggsw_sz;
     const uint32_t gbytes = (uint32_t)((size_t)(PBS ? n : n_in) * ggsw_sz * sizeof(cplx));
     const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc((void *)gbase, (short)0, gbytes, 0x00020000);
@@ -239,10 +245,11 @@ __global__ void __launch_bounds__(THREADS, 1)
                     v[m] = {fma(a0, tw.re, -(a1 * tw.im)), fma(a0, tw.im, a1 * tw.re)};
                 }
                 dft8<false>(v, w81, w83);
+                X[pidx(tt)] = v[0];
 #pragma unroll
-                for (int kk = 0; kk < 8; kk++) {
-                    const cplx tv = cmul(v[kk], s_w[tt * kk]);
-                    X[pidx(tt + 64 * kk)] = csel(tt * kk != 0, tv, v[kk]);
+                for (int kk = 1; kk < 8; kk++) {
+                    const cplx tv = cmul(v[kk], s_w0[(kk - 1) * 64 + tt]);
+                    X[pidx(tt + 64 * kk)] = csel(tt != 0, tv, v[kk]);
                 }
                 wave_sync();
                 if (lev == LEV) s_setprio_c<1>(); else s_setprio_c<2>();
@@ -252,10 +259,11 @@ __global__ void __launch_bounds__(THREADS, 1)
 #pragma unroll
                     for (int m = 0; m < 8; m++) v[m] = X[pidx(64 * gg + uu + 8 * m)];
                     dft8<false>(v, w81, w83);
+                    X[pidx(64 * gg + uu)] = v[0];
 #pragma unroll
-                    for (int kk = 0; kk < 8; kk++) {
-                        const cplx tv = cmul(v[kk], s_w[8 * uu * kk]);
-                        X[pidx(64 * gg + uu + 8 * kk)] = csel(uu * kk != 0, tv, v[kk]);
+                    for (int kk = 1; kk < 8; kk++) {
+                        const cplx tv = cmul(v[kk], s_w1[(kk - 1) * 8 + uu]);
+                        X[pidx(64 * gg + uu + 8 * kk)] = csel(uu != 0, tv, v[kk]);
                     }
                 }
                 wave_sync();
@@ -317,11 +325,12 @@ __global__ void __launch_bounds__(THREADS, 1)
             // inverse pass 1: conj(w[8 uu kk]) on points 64 gg + uu + 8 kk
             {
                 const int gg = tt >> 3, uu = tt & 7;
+                v[0] = Y[pidx(64 * gg + uu)];
 #pragma unroll
-                for (int kk = 0; kk < 8; kk++) {
+                for (int kk = 1; kk < 8; kk++) {
                     const cplx y = Y[pidx(64 * gg + uu + 8 * kk)];
-                    const cplx tv = cmul(y, cconj(s_w[8 * uu * kk]));
-                    v[kk] = csel(uu * kk != 0, tv, y);
+                    const cplx tv = cmul(y, cconj(s_w1[(kk - 1) * 8 + uu]));
+                    v[kk] = csel(uu != 0, tv, y);
                 }
                 dft8<true>(v, w81, w83);
 #pragma unroll
@@ -330,11 +339,12 @@ __global__ void __launch_bounds__(THREADS, 1)
             wave_sync();
             s_setprio_c<2>();
             // inverse pass 0: conj(w[t kk]) on points t + 64 kk, untwist, from_torus, ACC +=
+            v[0] = Y[pidx(tt)];
 #pragma unroll
-            for (int kk = 0; kk < 8; kk++) {
+            for (int kk = 1; kk < 8; kk++) {
                 const cplx y = Y[pidx(tt + 64 * kk)];
-                const cplx tv = cmul(y, cconj(s_w[tt * kk]));
-                v[kk] = csel(tt * kk != 0, tv, y);
+                const cplx tv = cmul(y, cconj(s_w0[(kk - 1) * 64 + tt]));
+                v[kk] = csel(tt != 0, tv, y);
             }
             dft8<true>(v, w81, w83);
             uint64_t *poly = acc + jb * ACC_STRIDE;
@@ -374,7 +384,9 @@ __global__ void __launch_bounds__(THREADS, 1)
     }
 }
 
-inline size_t lds_bytes() { return (size_t)JOBS * ACC_STRIDE * 8 + (size_t)JOBS * BUF_STRIDE * 16 + 3 * (size_t)M * 16; }
+inline size_t lds_bytes() {
+    return (size_t)JOBS * ACC_STRIDE * 8 + (size_t)JOBS * BUF_STRIDE * 16 + 3 * (size_t)M * 16 + (7 * 64 + 7 * 8) * 16;
+}
 
 // (levels, base_log) combinations of the N=1024 parameter sets: returns the kernel or nullptr
 typedef void (*kernel_t)(const uint64_t *, int, const uint64_t *, int, const cplx *, int, uint64_t *, long, uint64_t,
