@@ -31,6 +31,7 @@ README_KEY = bytes.fromhex("76b8e0ada0f13d90405d6ae55386bd28")  # README / main.
 README_IV = bytes.fromhex("bdd219b8a08ded1a")
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (= FP64 matrix) dense peak, spec
+FP64_SUSTAINED_TFLOPS = 58.0  # measured sustained v_fma_f64 rate, all CUs (scripts/probes/fp64_peak.hip)
 PBS_KERNELS = {"1bit": "tae::br512x4::br_kernel<3, true, 12>", "8bit": "tae::br1024::br_kernel<6, true, 7>"}
 
 
@@ -259,7 +260,10 @@ def main():
                           "note": "whole PBS stage per launch: the kernel above + the br512lat remainder"},
                 "hbm": {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": (gbs / HBM_PEAK_GBS) if gbs else None,
-                        "algorithmic_bytes_per_launch": k_bytes}}
+                        "algorithmic_bytes_per_launch": k_bytes},
+                "sustained": {"peak": FP64_SUSTAINED_TFLOPS, "frac": (tflops / FP64_SUSTAINED_TFLOPS) if tflops else None,
+                              "note": "v_fma_f64 rate the chip holds with every CU busy "
+                                      "(scripts/probes/fp64_peak.hip); the spec peak assumes 2.4 GHz"}}
     stage_share = {k: v / args.steps for k, v in stage_ms.items() if k not in ("pbs_launches", "pbs_main_cts")}
 
     cpu = None
