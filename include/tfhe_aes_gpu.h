@@ -44,7 +44,10 @@ extern "C" {
  * is bootstrapped through one 8-bit integer ciphertext (big key, [K+1], plaintext m * 2^56). */
 #define TAE_PARAMS_WOPPBS_8BIT 4
 
-/* memory kinds for the raw-array entry points */
+/* memory kinds for the raw-array entry points.  TAE_MEM_DEVICE: pointers into the context's device
+ * memory.  The library orders itself after all work already queued on that device (it synchronizes
+ * the device before its first read of caller buffers, e.g. after an RCCL broadcast or torch copies
+ * on other streams), and device outputs are complete when the call returns. */
 #define TAE_MEM_HOST 0
 #define TAE_MEM_DEVICE 1
 
