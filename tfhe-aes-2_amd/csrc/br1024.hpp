@@ -25,7 +25,7 @@ __device__ __forceinline__ void s_setprio_c() {
 #endif
 }
 
-constexpr int N = 1024, M = 512, K1 = 3, C = 2, JOBS = C * K1, THREADS = 512;
+constexpr int N = 1024, M = 512, K1 = 3, THREADS = 512;
 
 // TAE_B1K_PROF (debug builds only): per-phase cycle sums of every wave of workgroup 0
 #ifdef TAE_B1K_PROF
@@ -79,13 +79,16 @@ __device__ __forceinline__ void dft8(cplx *v, cplx w1, cplx w3) {
 
 // Mode: PBS -> GGSW_i = bsk + i * ggsw_sz, per-ciphertext rotation a~_i; steps = n.
 //       VP  -> GGSW_t = ggsw_f + (g * n_in + b) * ggsw_sz, rotation X^{-2^t} shared; steps = n_in.
-template <int LEV, bool PBS, int BLOG>
+// C ciphertexts per workgroup: 2 (6 FFT jobs on 8 waves, GGSW loads shared by both) for batches that
+// fill the chip, 1 (3 jobs, one per SIMD) for small batches -- e.g. the 8-bit model's extract_bits
+// rounds of one byte per block, where C = 2 would leave half the CUs idle
+template <int LEV, bool PBS, int BLOG, int C>
 __global__ void __launch_bounds__(THREADS, 1)
     br_kernel(const uint64_t *__restrict__ lwe_in, int n, const uint64_t *__restrict__ lut, int n_out,
               const cplx *__restrict__ ggsw_base, int n_in, uint64_t *__restrict__ out, long B,
               uint64_t body_add, uint64_t out_add, const cplx *__restrict__ twist, const cplx *__restrict__ untwist,
               const cplx *__restrict__ wtab) {
-    constexpr int LOGN = 10;
+    constexpr int LOGN = 10, JOBS = C * K1;
     extern __shared__ __align__(16) unsigned char smem[];
     uint64_t *acc = reinterpret_cast<uint64_t *>(smem);             // [JOBS][ACC_STRIDE]
     cplx *buf = reinterpret_cast<cplx *>(acc + JOBS * ACC_STRIDE);  // [JOBS][BUF_STRIDE]
@@ -384,17 +387,18 @@ __global__ void __launch_bounds__(THREADS, 1)
     }
 }
 
-inline size_t lds_bytes() {
-    return (size_t)JOBS * ACC_STRIDE * 8 + (size_t)JOBS * BUF_STRIDE * 16 + 3 * (size_t)M * 16 + (7 * 64 + 7 * 8) * 16;
+inline size_t lds_bytes(int C) {
+    return (size_t)C * K1 * ACC_STRIDE * 8 + (size_t)C * K1 * BUF_STRIDE * 16 + 3 * (size_t)M * 16 + (7 * 64 + 7 * 8) * 16;
 }
 
 // (levels, base_log) combinations of the N=1024 parameter sets: returns the kernel or nullptr
 typedef void (*kernel_t)(const uint64_t *, int, const uint64_t *, int, const cplx *, int, uint64_t *, long, uint64_t,
                          uint64_t, const cplx *, const cplx *, const cplx *);
+template <int C>
 inline kernel_t pick(bool pbs, int levels, int base_log) {
-#define TAE_BR1024(L, BL)                                                          \
-    if (levels == L && base_log == BL)                                             \
-        return pbs ? (kernel_t)br_kernel<L, true, BL> : (kernel_t)br_kernel<L, false, BL>;
+#define TAE_BR1024(L, BL)                                                                \
+    if (levels == L && base_log == BL)                                                   \
+        return pbs ? (kernel_t)br_kernel<L, true, BL, C> : (kernel_t)br_kernel<L, false, BL, C>;
     TAE_BR1024(6, 7)   // 8-bit model PBS (shortint_woppbs_8bit.rs:39-86)
     TAE_BR1024(4, 6)   // 8-bit model CBS GGSW
     TAE_BR1024(2, 15)  // params_sqrd_lvl_1 / _4 PBS

@@ -640,12 +640,16 @@ void Engine::init_common() {
     }
     // batched N=1024, k=2 blind rotation (br1024.hpp); other shapes run the generic kernels
     if (p_.N == 1024 && p_.k == 2) {
-        br1024_pbs_ = br1024::pick(true, p_.pbs_l, p_.pbs_b);
-        br1024_vp_ = br1024::pick(false, p_.cbs_l, p_.cbs_b);
+        br1024_pbs_ = br1024::pick<2>(true, p_.pbs_l, p_.pbs_b);
+        br1024_pbs1_ = br1024::pick<1>(true, p_.pbs_l, p_.pbs_b);
+        br1024_vp_ = br1024::pick<2>(false, p_.cbs_l, p_.cbs_b);
         for (auto kf : {br1024_pbs_, br1024_vp_})
             if (kf)
                 HIPC(hipFuncSetAttribute((const void *)kf, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)br1024::lds_bytes()));
+                                         (int)br1024::lds_bytes(2)));
+        if (br1024_pbs1_)
+            HIPC(hipFuncSetAttribute((const void *)br1024_pbs1_, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)br1024::lds_bytes(1)));
     }
     // opt-in to >64 KiB dynamic LDS for the blind-rotation kernels
     if (p_.N == 512) {
@@ -841,8 +845,10 @@ void Engine::bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint
         return;
     }
     if (br1024_pbs_) {
-        const size_t wgs = (B + br1024::C - 1) / br1024::C;
-        br1024_pbs_<<<(unsigned)wgs, br1024::THREADS, br1024::lds_bytes(), stream_>>>(
+        // two ciphertexts per workgroup share its GGSW loads, but below one per CU they leave CUs idle
+        const int C = (long)B <= (long)num_cu_ ? 1 : 2;
+        const size_t wgs = (B + C - 1) / C;
+        (C == 1 ? br1024_pbs1_ : br1024_pbs_)<<<(unsigned)wgs, br1024::THREADS, br1024::lds_bytes(C), stream_>>>(
             d_small, p_.n, d_lut_glwe, 0, d_bsk_f_, 0, d_big, (long)B, body_add, out_add, d_twist_, d_untwist_, d_w_);
         HIPC(hipGetLastError());
         return;
@@ -985,8 +991,8 @@ void Engine::vertical_packing(const cplx *d_ggsw_f, size_t G, int n_in, const ui
         return;
     }
     if (br1024_vp_) {
-        const size_t wgs = G * (size_t)((n_out + br1024::C - 1) / br1024::C);
-        br1024_vp_<<<(unsigned)wgs, br1024::THREADS, br1024::lds_bytes(), stream_>>>(
+        const size_t wgs = G * (size_t)((n_out + 1) / 2);
+        br1024_vp_<<<(unsigned)wgs, br1024::THREADS, br1024::lds_bytes(2), stream_>>>(
             nullptr, 0, d_lut, n_out, d_ggsw_f, n_in, d_out, (long)G, 0, 0, d_twist_, d_untwist_, d_w_);
         HIPC(hipGetLastError());
         return;
