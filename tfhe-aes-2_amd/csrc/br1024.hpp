@@ -81,17 +81,21 @@ __device__ __forceinline__ void dft8(cplx *v, cplx w1, cplx w3) {
 //       VP  -> GGSW_t = ggsw_f + (g * n_in + b) * ggsw_sz, rotation X^{-2^t} shared; steps = n_in.
 // C ciphertexts per workgroup: 2 (6 FFT jobs on 8 waves, GGSW loads shared by both) for batches that
 // fill the chip, 1 (3 jobs, one per SIMD) for small batches -- e.g. the 8-bit model's extract_bits
-// rounds of one byte per block, where C = 2 would leave half the CUs idle
-template <int LEV, bool PBS, int BLOG, int C>
+// rounds of one byte per block, where C = 2 would leave half the CUs idle.  LP levels per pass: with
+// C = 1 and an even level count, LP = 2 runs the FFTs of two decomposition levels together (6 jobs on
+// 8 waves instead of 3), halving the level passes and their barriers; the MAC still consumes the
+// levels in descending order.
+template <int LEV, bool PBS, int BLOG, int C, int LP>
 __global__ void __launch_bounds__(THREADS, 1)
     br_kernel(const uint64_t *__restrict__ lwe_in, int n, const uint64_t *__restrict__ lut, int n_out,
               const cplx *__restrict__ ggsw_base, int n_in, uint64_t *__restrict__ out, long B,
               uint64_t body_add, uint64_t out_add, const cplx *__restrict__ twist, const cplx *__restrict__ untwist,
               const cplx *__restrict__ wtab) {
-    constexpr int LOGN = 10, JOBS = C * K1;
+    static_assert(LEV % LP == 0, "levels per pass must divide the level count");
+    constexpr int LOGN = 10, CJ = C * K1, JOBS = CJ * LP;
     extern __shared__ __align__(16) unsigned char smem[];
-    uint64_t *acc = reinterpret_cast<uint64_t *>(smem);             // [JOBS][ACC_STRIDE]
-    cplx *buf = reinterpret_cast<cplx *>(acc + JOBS * ACC_STRIDE);  // [JOBS][BUF_STRIDE]
+    uint64_t *acc = reinterpret_cast<uint64_t *>(smem);           // [CJ][ACC_STRIDE]
+    cplx *buf = reinterpret_cast<cplx *>(acc + CJ * ACC_STRIDE);  // [JOBS][BUF_STRIDE], job = (lh, ct, p)
     cplx *s_tw = buf + JOBS * BUF_STRIDE;                           // twist
     cplx *s_w = s_tw + M;                                           // W_512 table
     cplx *s_utw = s_w + M;                                          // untwist = conj(twist) / M
@@ -103,7 +107,9 @@ __global__ void __launch_bounds__(THREADS, 1)
     const int jb = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int t = tid & 63;
     const bool fjob = jb < JOBS;
-    const int jct = fjob ? jb / K1 : 0;
+    const int jcp = fjob ? jb % CJ : 0;  // (ct, p) of the job
+    const int jlh = fjob ? jb / CJ : 0;  // level offset inside a pass
+    const int jct = jcp / K1;
     const size_t ggsw_sz = (size_t)LEV * K1 * K1 * M;
 
     long ct0, g = 0;
@@ -132,7 +138,7 @@ __global__ void __launch_bounds__(THREADS, 1)
     const int pos = tid;  // MAC: Fourier position
     const int gvoff = pos * (int)sizeof(cplx);
 
-    for (int i = tid; i < JOBS * N; i += THREADS) {
+    for (int i = tid; i < CJ * N; i += THREADS) {
         const int job = i / N, j = i - job * N;
         const int ct = job / K1, c = job - ct * K1;
         uint64_t v = 0;
@@ -154,7 +160,7 @@ __global__ void __launch_bounds__(THREADS, 1)
     const int steps = PBS ? n : n_in;
     uint64_t a_next = (PBS && jvalid) ? lwe_in[(size_t)(ct0 + jct) * (n + 1)] : 0;
     cplx accr[K1 * C];
-    cplx gv[K1 * K1];
+    cplx gv[LP * K1 * K1];
     BPROF_DECL
     for (int step = 0; step < steps; step++) {
         s_setprio_c<2>();
@@ -178,7 +184,7 @@ __global__ void __launch_bounds__(THREADS, 1)
         constexpr int DW = BYTES ? (LEV + 1) / 2 : LEV;
         uint32_t dig[DW][8];
         if (fjob) {
-            const uint64_t *poly = acc + jb * ACC_STRIDE;
+            const uint64_t *poly = acc + jcp * ACC_STRIDE;
             const int bt = tt - e;
 #pragma unroll
             for (int m = 0; m < 8; m++) {
@@ -209,17 +215,19 @@ __global__ void __launch_bounds__(THREADS, 1)
 #pragma unroll
         for (int a = 0; a < K1 * C; a++) accr[a] = cplx{0.0, 0.0};
 
-#pragma unroll(LEV <= 2 ? LEV : 1)
         BPROF(0);
-        for (int lev = LEV; lev >= 1; lev--) {
+        for (int lev0 = LEV; lev0 >= 1; lev0 -= LP) {
 #pragma unroll
-            for (int p = 0; p < K1; p++)
+            for (int lh = 0; lh < LP; lh++)
 #pragma unroll
-                for (int q = 0; q < K1; q++) {
-                    const int soff = gstep + (((lev - 1) * K1 + p) * K1 + q) * M * (int)sizeof(cplx);
-                    const u32x4 rv = __builtin_amdgcn_raw_buffer_load_b128(grs, gvoff, soff, 0);
-                    __builtin_memcpy(&gv[p * K1 + q], &rv, sizeof(cplx));
-                }
+                for (int p = 0; p < K1; p++)
+#pragma unroll
+                    for (int q = 0; q < K1; q++) {
+                        const int soff = gstep + (((lev0 - lh - 1) * K1 + p) * K1 + q) * M * (int)sizeof(cplx);
+                        const u32x4 rv = __builtin_amdgcn_raw_buffer_load_b128(grs, gvoff, soff, 0);
+                        __builtin_memcpy(&gv[(lh * K1 + p) * K1 + q], &rv, sizeof(cplx));
+                    }
+            const int lev = lev0 - jlh;  // this wave's level
             if (fjob) {
                 cplx *X = buf + jb * BUF_STRIDE;
                 cplx v[8];
@@ -255,7 +263,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                     X[pidx(tt + 64 * kk)] = csel(tt != 0, tv, v[kk]);
                 }
                 wave_sync();
-                if (lev == LEV) s_setprio_c<1>(); else s_setprio_c<2>();
+                if (lev0 == LEV) s_setprio_c<1>(); else s_setprio_c<2>();
                 // pass 1: points 64 gg + uu + 8 m, w[8 uu kk]
                 {
                     const int gg = tt >> 3, uu = tt & 7;
@@ -270,7 +278,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                     }
                 }
                 wave_sync();
-                if (lev == LEV) s_setprio_c<0>(); else s_setprio_c<1>();
+                if (lev0 == LEV) s_setprio_c<0>(); else s_setprio_c<1>();
                 // pass 2: points 8 t + m, no twiddles
 #pragma unroll
                 for (int m = 0; m < 8; m++) v[m] = X[pidx(8 * tt + m)];
@@ -282,19 +290,20 @@ __global__ void __launch_bounds__(THREADS, 1)
             br512::lds_sync();
             BPROF(2);
             s_setprio_c<3>();
-            // MAC at Fourier position pos: accumulator (q, c) = accr[q * C + c], p ascending
+            // MAC at Fourier position pos: accumulator (q, c) = accr[q * C + c]; levels descending, p ascending
 #pragma unroll
-            for (int p = 0; p < K1; p++) {
-                if (p == 1) s_setprio_c<2>();
-                if (p == 2) s_setprio_c<1>();
+            for (int lp = 0; lp < LP * K1; lp++) {
+                const int lh = lp / K1, p = lp - lh * K1;
+                if (lp == LP * K1 / 3) s_setprio_c<2>();
+                if (lp == 2 * LP * K1 / 3) s_setprio_c<1>();
                 cplx x[C];
 #pragma unroll
-                for (int c = 0; c < C; c++) x[c] = buf[(c * K1 + p) * BUF_STRIDE + pidx(pos)];
+                for (int c = 0; c < C; c++) x[c] = buf[((lh * C + c) * K1 + p) * BUF_STRIDE + pidx(pos)];
 #pragma unroll
                 for (int q = 0; q < K1; q++)
 #pragma unroll
                     for (int c = 0; c < C; c++) {
-                        const cplx gg = gv[p * K1 + q];
+                        const cplx gg = gv[lp * K1 + q];
                         double re = accr[q * C + c].re, im = accr[q * C + c].im;
                         re = fma(x[c].re, gg.re, re);
                         re = fma(-x[c].im, gg.im, re);
@@ -315,7 +324,7 @@ __global__ void __launch_bounds__(THREADS, 1)
             for (int c = 0; c < C; c++) buf[(c * K1 + q) * BUF_STRIDE + pidx(pos)] = accr[q * C + c];
         br512::lds_sync();
         s_setprio_c<3>();
-        if (fjob) {
+        if (jb < CJ) {
             cplx *Y = buf + jb * BUF_STRIDE;
             cplx v[8];
             // inverse pass 2: points 8 t + kk, no twiddles
@@ -365,7 +374,9 @@ __global__ void __launch_bounds__(THREADS, 1)
                 poly[j + M] = a1;
             }
         }
-        wave_sync();
+        // LP > 1: the second-level waves decompose polynomials the first-level waves just updated
+        if constexpr (LP > 1) br512::lds_sync();
+        else wave_sync();
         BPROF(4);
     }
 #ifdef TAE_B1K_PROF
@@ -387,18 +398,23 @@ __global__ void __launch_bounds__(THREADS, 1)
     }
 }
 
-inline size_t lds_bytes(int C) {
-    return (size_t)C * K1 * ACC_STRIDE * 8 + (size_t)C * K1 * BUF_STRIDE * 16 + 3 * (size_t)M * 16 + (7 * 64 + 7 * 8) * 16;
+inline size_t lds_bytes(int C, int LP = 1) {
+    return (size_t)C * K1 * ACC_STRIDE * 8 + (size_t)C * K1 * LP * BUF_STRIDE * 16 + 3 * (size_t)M * 16 +
+           (7 * 64 + 7 * 8) * 16;
 }
 
 // (levels, base_log) combinations of the N=1024 parameter sets: returns the kernel or nullptr
 typedef void (*kernel_t)(const uint64_t *, int, const uint64_t *, int, const cplx *, int, uint64_t *, long, uint64_t,
                          uint64_t, const cplx *, const cplx *, const cplx *);
-template <int C>
+// LP levels per pass; LP = 2 only for the PBS with at least two passes (nullptr otherwise)
+template <int C, int LP = 1>
 inline kernel_t pick(bool pbs, int levels, int base_log) {
-#define TAE_BR1024(L, BL)                                                                \
-    if (levels == L && base_log == BL)                                                   \
-        return pbs ? (kernel_t)br_kernel<L, true, BL, C> : (kernel_t)br_kernel<L, false, BL, C>;
+#define TAE_BR1024(L, BL)                                                                                  \
+    if constexpr (LP == 1)                                                                                 \
+        if (levels == L && base_log == BL)                                                                 \
+            return pbs ? (kernel_t)br_kernel<L, true, BL, C, LP> : (kernel_t)br_kernel<L, false, BL, C, LP>; \
+    if constexpr (LP == 2 && L % 2 == 0 && L >= 4)                                                         \
+        if (pbs && levels == L && base_log == BL) return (kernel_t)br_kernel<L, true, BL, C, LP>;
     TAE_BR1024(6, 7)   // 8-bit model PBS (shortint_woppbs_8bit.rs:39-86)
     TAE_BR1024(4, 6)   // 8-bit model CBS GGSW
     TAE_BR1024(2, 15)  // params_sqrd_lvl_1 / _4 PBS

@@ -177,6 +177,7 @@ class Engine {
                         uint64_t, const cplx *, const cplx *, const cplx *) = nullptr;
     decltype(br1024_pbs_) br1024_vp_ = nullptr;
     decltype(br1024_pbs_) br1024_pbs1_ = nullptr;  // one ciphertext per workgroup (small batches)
+    int br1024_pbs1_lp_ = 1;                       // its levels per pass
     bool x4_512_ = false;     // N = 512, k = 4 (lvl_64): batched blind rotations br512x4 / br512lat
     long lat_max_ = 256;      // batch size up to which br512lat runs (TAE_BR_LAT_MAX)
     int num_cu_ = 256;

@@ -641,7 +641,14 @@ void Engine::init_common() {
     // batched N=1024, k=2 blind rotation (br1024.hpp); other shapes run the generic kernels
     if (p_.N == 1024 && p_.k == 2) {
         br1024_pbs_ = br1024::pick<2>(true, p_.pbs_l, p_.pbs_b);
-        br1024_pbs1_ = br1024::pick<1>(true, p_.pbs_l, p_.pbs_b);
+        // one ciphertext per workgroup: two levels per pass where the level count allows (TAE_B1K_PAIR=0: one)
+        const char *pair = getenv("TAE_B1K_PAIR");
+        br1024_pbs1_lp_ = (pair && pair[0] == '0') ? 1 : 2;
+        br1024_pbs1_ = br1024_pbs1_lp_ == 2 ? br1024::pick<1, 2>(true, p_.pbs_l, p_.pbs_b) : nullptr;
+        if (!br1024_pbs1_) {
+            br1024_pbs1_lp_ = 1;
+            br1024_pbs1_ = br1024::pick<1>(true, p_.pbs_l, p_.pbs_b);
+        }
         br1024_vp_ = br1024::pick<2>(false, p_.cbs_l, p_.cbs_b);
         for (auto kf : {br1024_pbs_, br1024_vp_})
             if (kf)
@@ -649,7 +656,7 @@ void Engine::init_common() {
                                          (int)br1024::lds_bytes(2)));
         if (br1024_pbs1_)
             HIPC(hipFuncSetAttribute((const void *)br1024_pbs1_, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)br1024::lds_bytes(1)));
+                                     (int)br1024::lds_bytes(1, br1024_pbs1_lp_)));
     }
     // opt-in to >64 KiB dynamic LDS for the blind-rotation kernels
     if (p_.N == 512) {
@@ -848,7 +855,8 @@ void Engine::bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint
         // two ciphertexts per workgroup share its GGSW loads, but below one per CU they leave CUs idle
         const int C = (long)B <= (long)num_cu_ ? 1 : 2;
         const size_t wgs = (B + C - 1) / C;
-        (C == 1 ? br1024_pbs1_ : br1024_pbs_)<<<(unsigned)wgs, br1024::THREADS, br1024::lds_bytes(C), stream_>>>(
+        (C == 1 ? br1024_pbs1_ : br1024_pbs_)<<<(unsigned)wgs, br1024::THREADS, br1024::lds_bytes(C, C == 1 ? br1024_pbs1_lp_ : 1),
+                                                              stream_>>>(
             d_small, p_.n, d_lut_glwe, 0, d_bsk_f_, 0, d_big, (long)B, body_add, out_add, d_twist_, d_untwist_, d_w_);
         HIPC(hipGetLastError());
         return;
