@@ -71,6 +71,8 @@ def main():
                          "(--model8-blocks blocks, one step) and report it beside the headline line; auto = on "
                          "at world size 1")
     ap.add_argument("--model8-blocks", type=int, default=16)
+    ap.add_argument("--host-buffers", choices=["auto", "on", "off"], default="auto",
+                    help="one extra step with host arrays (PCIe-inclusive rate); auto = on at world 1")
     args = ap.parse_args()
     PBS_KERNEL = PBS_KERNELS[args.model]
 
@@ -215,6 +217,19 @@ def main():
                   "correct": got1 == aes_128.encrypt_block_plain(aes_128.key_schedule_plain(README_KEY), blocks[0],
                                                                  args.rounds)}
 
+    # ---- host buffers: one step through tae_aes_encrypt_blocks_raw with host arrays (PCIe copies of
+    # the expanded key, blocks and results included); reported beside `value`, never as it ----
+    host_io = None
+    if args.host_buffers == "on" or (args.host_buffers == "auto" and world == 1):
+        blocks_h = cts.reshape(nb, 128, L)
+        t1 = time.time()
+        out_h = E.encrypt_blocks_raw(ctx, rk_np, blocks_h, args.rounds)
+        dt = time.time() - t1
+        host_io = {"config": f"{nb} blocks x {args.rounds} rounds, host arrays in and out (one step)",
+                   "s_per_step": dt, "blocks_per_s": nb / dt,
+                   "copy_bytes": int(rk_np.nbytes + blocks_h.nbytes + out_h.nbytes),
+                   "identical_to_device_path": bool(np.array_equal(out_h.reshape(out.shape), out))}
+
     total_blocks = nb * world * args.steps
     value = total_blocks / elapsed
     ms_per_step = elapsed * 1000.0 / args.steps
@@ -290,7 +305,8 @@ def main():
                "roofline": roofline, "cpu_baseline": cpu,
                "stage_ms_per_step": stage_share, "per_sbox_ms": ms_per_step / (nb * 16 * args.rounds),
                "keygen_s": keygen_s, "key_setup_s": key_setup_s, "key_expansion_s": key_expansion_s,
-               "encrypt_s": encrypt_s, "correct": bool(ok), "single_block": single, "model8": model8}
+               "encrypt_s": encrypt_s, "correct": bool(ok), "single_block": single, "host_buffers": host_io,
+               "model8": model8}
         print(json.dumps(rec), flush=True)
     if dist:
         dist.destroy_process_group()

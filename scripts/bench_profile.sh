@@ -13,7 +13,7 @@ timeout -k 10 ${BENCH_TIMEOUT:-900} python "$ROOT/bench.py" --steps $STEPS --war
 cat "$OUT/bench.json"
 [ "${PROFILE:-1}" = "1" ] || exit 0
 cd /tmp && export TMPDIR=/tmp
-ARGS="--steps 1 --warmup 0 --cpu-baseline off --single-block off --model8-leg off --key-schedule plain --blocks-per-gpu $BLOCKS"
+ARGS="--steps 1 --warmup 0 --cpu-baseline off --single-block off --model8-leg off --host-buffers off --key-schedule plain --blocks-per-gpu $BLOCKS"
 T=${PROF_TIMEOUT:-600}
 timeout -k 10 $T rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" $ARGS > "$OUT/prof_bench.json" 2> "$OUT/prof.err" || { echo "rocprof failed rc=$?"; tail -30 "$OUT/prof.err"; exit 1; }
 if [ "${PMC:-1}" = "1" ]; then
