@@ -8,6 +8,14 @@ import sys
 
 import pytest
 
+# PyTorch-ROCm bundles its own HIP runtime under the same soname as /opt/rocm's; whichever is loaded
+# first serves the whole process, and torch cannot start on the other one.  Load torch's first, as
+# bench.py does, so that tests which move keys to the GPU with torch work in any selection.
+try:
+    import torch  # noqa: F401
+except ImportError:
+    pass
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "tfhe-aes-2_amd")
 for p in (ROOT, PKG):

@@ -1,6 +1,7 @@
-"""The integer-only torus helpers of the blind-rotation kernels (fft_device.hpp from_torus_bits,
-decompose16), compiled for the host and compared with the CPU oracle's tfhe-rs restatement
-(or_from_torus, or_decompose) on random and edge-case inputs (tests/native/torus_helpers_test.cpp)."""
+"""Host-compiled checks of device helpers: the integer-only torus helpers of the blind-rotation kernels
+(fft_device.hpp from_torus_bits, decompose16) against the CPU oracle's tfhe-rs restatement
+(or_from_torus, or_decompose) on random and edge-case inputs (tests/native/torus_helpers_test.cpp), and
+the K-layout PFKS slot plan (kslots.hpp, tests/native/kslots_test.cpp)."""
 import os
 import subprocess
 
@@ -15,5 +16,16 @@ def test_torus_helpers_match_oracle(tmp_path):
                     os.path.join(ROOT, "oracle", "build", "liboracle.so"), "-o", exe,
                     "-Wl,-rpath," + os.path.join(ROOT, "oracle", "build")], check=True)
     r = subprocess.run([exe, "1000000"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "OK" in r.stdout
+
+
+def test_pfks_slot_plan(tmp_path):
+    """K-layout PFKS slot plan (csrc/kslots.hpp): digit ranges, exact limb split of every digit and the
+    pre-shifted-key identity, on the base 2^16 x 2 and 2^12 x 3 shapes (tests/native/kslots_test.cpp)."""
+    exe = str(tmp_path / "kslots_test")
+    subprocess.run(["g++", "-O2", "-std=c++17", os.path.join(ROOT, "tests", "native", "kslots_test.cpp"), "-o", exe],
+                   check=True)
+    r = subprocess.run([exe, "2000000"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "OK" in r.stdout

@@ -307,32 +307,12 @@ __global__ void __launch_bounds__(256) prep_digits_kl(const uint64_t *__restrict
     const long b = t / n_in;
     const int i = (int)(t - b * n_in);
     if (b >= B) return;
-    const uint64_t x = in[b * in_stride + i];
-    const int nrb = 64 - base_log * levels;
-    uint64_t s = x >> (nrb - 1);
-    s += s & 1;
-    s >>= 1;
-    const uint64_t mask = (1ull << base_log) - 1;
-    for (int lev = levels; lev >= 1; lev--) {
-        const uint64_t res = s & mask;
-        s >>= base_log;
-        uint64_t carry = ((res - 1) | s) & res;
-        carry >>= (base_log - 1);
-        s += carry;
-        int64_t d = (int64_t)(res - (carry << base_log)) - ks.off[lev - 1];
+    kl_for_each_digit(in[b * in_stride + i], base_log, levels, [&](int lev, int64_t digit) {
+        int64_t d = digit - ks.off[lev - 1];
         const int n = ks.nlimb[lev - 1];
         const long k0 = (long)i * ks.S + ks.first[lev - 1];
-        for (int m = 0; m < n; m++) {
-            int64_t limb;
-            if (m == n - 1) {
-                limb = d;
-            } else {
-                limb = ((d + 128) & 255) - 128;
-                d = (d - limb) >> 8;
-            }
-            A[op_off(b, k0 + m, Kp, true)] = (int8_t)limb;
-        }
-    }
+        for (int m = 0; m < n; m++) A[op_off(b, k0 + m, Kp, true)] = (int8_t)kl_next_limb(d, m == n - 1);
+    });
 }
 
 // key rows in the K layout (prep_key with the slot shift): element (kd = i * L + l, col) of the u64

@@ -4,6 +4,12 @@
 #pragma once
 #include <cstdint>
 
+#if defined(__HIPCC__)
+#define TAE_KS_HD __host__ __device__
+#else
+#define TAE_KS_HD
+#endif
+
 namespace tae {
 namespace ksgemm {
 
@@ -44,6 +50,34 @@ inline bool kslots_build(int base_log, int levels, KSlots &ks) {
         }
     }
     return true;
+}
+
+// The balanced digits of x (tfhe-rs SignedDecomposer: closest representable, then the carry rule of
+// decompose_one_level), least significant level first: f(lev, digit) for lev = levels .. 1.
+template <class F>
+TAE_KS_HD inline void kl_for_each_digit(uint64_t x, int base_log, int levels, F &&f) {
+    const int nrb = 64 - base_log * levels;
+    uint64_t s = x >> (nrb - 1);
+    s += s & 1;
+    s >>= 1;
+    const uint64_t mask = (1ull << base_log) - 1;
+    for (int lev = levels; lev >= 1; lev--) {
+        const uint64_t res = s & mask;
+        s >>= base_log;
+        uint64_t carry = ((res - 1) | s) & res;
+        carry >>= (base_log - 1);
+        s += carry;
+        f(lev, (int64_t)(res - (carry << base_log)));
+    }
+}
+
+// The next signed 8-bit limb of an offset digit d (least significant first; the last limb takes the
+// rest, which the slot plan keeps in [-128, 127]); d is left holding the limbs still to come.
+TAE_KS_HD inline int64_t kl_next_limb(int64_t &d, bool last) {
+    if (last) return d;
+    const int64_t limb = ((d + 128) & 255) - 128;
+    d = (d - limb) >> 8;
+    return limb;
 }
 
 }  // namespace ksgemm
