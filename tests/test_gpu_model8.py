@@ -58,16 +58,17 @@ def test_pbs_shift_boolean8_bit_exact(gpu_context8, oracle_keys8, client8, level
         assert min(err, (1 << 64) - err) < 1 << (63 - 6 * level), (i, level)  # within alpha
 
 
-@pytest.mark.parametrize("pair,B", [("1", 5), ("0", 5), ("1", 300)])
-def test_pbs8_kernel_variants_bit_exact(product_raw8, oracle_keys8, client8, pair, B):
-    """The br1024 blind-rotation variants the engine picks: one ciphertext per workgroup with two
-    levels per pass (default for batches up to one per CU) or one level per pass (TAE_B1K_PAIR=0), and
-    two ciphertexts per workgroup (B = 300 > the CU count, odd tail workgroup of one)."""
-    os.environ["TAE_B1K_PAIR"] = pair
+@pytest.mark.parametrize("lat,pair,B", [("1", "1", 5), ("0", "1", 5), ("0", "0", 5), ("1", "1", 300)])
+def test_pbs8_kernel_variants_bit_exact(product_raw8, oracle_keys8, client8, lat, pair, B):
+    """The N=1024 blind-rotation variants the engine picks: for batches up to one ciphertext per CU
+    the 1024-thread latency kernel (br1024lat, default), or with TAE_B1K_LAT=0 br1024 with one
+    ciphertext per workgroup and two levels per pass (or one: TAE_B1K_PAIR=0); and two ciphertexts
+    per workgroup (B = 300 > the CU count, odd tail workgroup of one)."""
+    os.environ["TAE_B1K_LAT"], os.environ["TAE_B1K_PAIR"] = lat, pair
     try:
         ctx = tfhe_aes.context_from_raw(tfhe_aes.PARAMS_WOPPBS_8BIT, product_raw8[1], device=0)
     finally:
-        del os.environ["TAE_B1K_PAIR"]
+        del os.environ["TAE_B1K_LAT"], os.environ["TAE_B1K_PAIR"]
     bits = np.random.default_rng(B).integers(0, 2, size=B).astype(np.uint8)
     small = client8.encrypt_bits_raw(bits, start_index=900)
     out = np.zeros((B, BIG), dtype=np.uint64)

@@ -178,6 +178,10 @@ class Engine {
     decltype(br1024_pbs_) br1024_vp_ = nullptr;
     decltype(br1024_pbs_) br1024_pbs1_ = nullptr;  // one ciphertext per workgroup (small batches)
     int br1024_pbs1_lp_ = 1;                       // its levels per pass
+    // latency blind rotation, one ciphertext per 1024-thread workgroup (br1024lat.hpp), or nullptr
+    void (*br1024lat_)(const uint64_t *, int, const uint64_t *, const cplx *, uint64_t *, long, uint64_t, uint64_t,
+                       const cplx *, const cplx *, const cplx *) = nullptr;
+    size_t br1024lat_lds_ = 0;
     bool x4_512_ = false;     // N = 512, k = 4 (lvl_64): batched blind rotations br512x4 / br512lat
     long lat_max_ = 256;      // batch size up to which br512lat runs (TAE_BR_LAT_MAX)
     int num_cu_ = 256;

@@ -22,6 +22,7 @@
 #include "br512x4.hpp"
 #include "br512lat.hpp"
 #include "br1024.hpp"
+#include "br1024lat.hpp"
 #include "ksgemm.hpp"
 #include "engine.hpp"
 #include "fft_device.hpp"
@@ -654,6 +655,15 @@ void Engine::init_common() {
             if (kf)
                 HIPC(hipFuncSetAttribute((const void *)kf, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          (int)br1024::lds_bytes(2)));
+        // one ciphertext per 1024-thread workgroup, three levels per pass (the 8-bit model's PBS;
+        // TAE_B1K_LAT=0: br1024's one-ciphertext kernel instead)
+        const char *blat = getenv("TAE_B1K_LAT");
+        if (p_.pbs_l == 6 && p_.pbs_b == 7 && !(blat && blat[0] == '0')) {
+            br1024lat_ = br1024lat::br_kernel<6, 7, 3>;
+            br1024lat_lds_ = br1024lat::lds_bytes<6, 7, 3>();
+            HIPC(hipFuncSetAttribute((const void *)br1024lat_, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)br1024lat_lds_));
+        }
         if (br1024_pbs1_)
             HIPC(hipFuncSetAttribute((const void *)br1024_pbs1_, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)br1024::lds_bytes(1, br1024_pbs1_lp_)));
@@ -849,6 +859,12 @@ void Engine::bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint
                 (long)B - bx, body_add, out_add, d_twist_, d_w_);
             HIPC(hipGetLastError());
         }
+        return;
+    }
+    if (br1024lat_ && (long)B <= (long)num_cu_) {
+        br1024lat_<<<(unsigned)B, br1024lat::THREADS, br1024lat_lds_, stream_>>>(
+            d_small, p_.n, d_lut_glwe, d_bsk_f_, d_big, (long)B, body_add, out_add, d_twist_, d_untwist_, d_w_);
+        HIPC(hipGetLastError());
         return;
     }
     if (br1024_pbs_) {
