@@ -1,7 +1,7 @@
 // Latency-oriented blind rotation for N = 512, k = 4 (small batches: one AES block is 128 bits):
 // ONE ciphertext per 1024-thread workgroup, and the decomposition LEVELS run in parallel instead
 // of one after another.  Wave jb < LEV * (k+1) owns FFT job (level jb / (k+1) + 1, polynomial
-// jb % (k+1)).  A CMux step is four barrier-separated phases:
+// jb % (k+1)).  A CMux step is five barrier-separated phases:
 //   D  decomposition of the rotated difference ACC * X^e - ACC of all k+1 polynomials, all levels
 //      at once, spread over all 16 waves (coefficient pairs (p, j), j < N/2), digits -> LDS
 //   F  forward FFT of all LEV * (k+1) digit polynomials (one wave each); the MAC's GGSW loads are
@@ -10,8 +10,10 @@
 //      waves 0-3 run two chains (q = 0 and 4) of one position, sharing its spectrum reads (holding
 //      the next level's rows in registers as well spills: 80 VGPRs of GGSW values alone; the level
 //      loop stays rolled, else the scheduler hoists all three levels' loads and spills)
-//   I  inverse FFT of the k+1 outputs (waves 0..k), untwist, torus conversion, ACC +=; the other
-//      waves issue the L2 prefetch of the GGSW rows two steps ahead, so that no phase waits on it
+//   I1 inverse FFT of the k+1 outputs (waves 0..k); the other waves issue the L2 prefetch of the
+//      GGSW rows two steps ahead, so that no phase waits on it
+//   I2 untwist, torus conversion and ACC += of the k+1 outputs spread over all 16 waves (in I1 they
+//      were a third of the inverse waves' VALU work, on a SIMD that runs two of the five jobs)
 // The per-phase profile of the previous layout (TAE_LAT_PROF) had the decomposition inside the
 // inverse phase (five waves, single-wave issue rate) and three dependent GGSW load rounds per MAC
 // chain behind the vmcnt of the prefetch loads.  The FFT jobs use br512x4's 4-lane DFT16
@@ -42,7 +44,7 @@ constexpr int THREADS = 1024;
 
 // TAE_LAT_PROF (debug builds only): per-phase cycle sums of every wave of workgroup 0
 #ifdef TAE_LAT_PROF
-#define LPROF_DECL uint64_t lprof_[8] = {0}, lprof_t_ = clock64();
+#define LPROF_DECL uint64_t lprof_[9] = {0}, lprof_t_ = clock64();
 #define LPROF(i)                           \
     do {                                   \
         asm volatile("" ::: "memory");     \
@@ -235,7 +237,8 @@ __global__ void __launch_bounds__(THREADS, 1)
         LPROF(4);
         lds_sync();
         LPROF(5);
-        // ---- I: inverse FFT of output q = jb, ACC += (waves 0..k); prefetch (the other waves) ----
+        // ---- I1: inverse FFT of output q = jb (waves 0..k), raw result -> obuf[q][j]; prefetch (the
+        // other waves) ----
         if (jb < K1) {
             cplx *base = obuf + jb * BUF_STRIDE;
             cplx v[4];
@@ -251,20 +254,9 @@ __global__ void __launch_bounds__(THREADS, 1)
                 v[i] = cmul(base[pidx(u + 16 * kk)], cconj(s_twa[16 * kk + u]));
             }
             dft16x4<true>(v, my_w16);
-            uint64_t *poly = acc + jb * N;
+            wave_sync();  // this wave's reads of base precede its writes below (LDS executes in order)
 #pragma unroll
-            for (int k2 = 0; k2 < 4; k2++) {
-                const int j = ll + 64 * k2;
-                const cplx t = cmul(v[k2], s_utw[j]);
-                bool o0, o1;
-                uint64_t a0 = torus_add_fast(t.re, poly[j], o0), a1 = torus_add_fast(t.im, poly[j + M], o1);
-                if (__builtin_amdgcn_ballot_w64(!(o0 && o1))) {  // zeros, out-of-range magnitudes (rare)
-                    a0 = poly[j] + from_torus_bits(t.re);
-                    a1 = poly[j + M] + from_torus_bits(t.im);
-                }
-                poly[j] = a0;
-                poly[j + M] = a1;
-            }
+            for (int k2 = 0; k2 < 4; k2++) base[ll + 64 * k2] = v[k2];  // coefficient pair j = ll + 64 k2
         } else if (step + 2 < n) {
 #pragma unroll
             for (int i = 0; i < PF; i++) {
@@ -279,16 +271,32 @@ __global__ void __launch_bounds__(THREADS, 1)
         }
         LPROF(6);
         lds_sync();
+        // ---- I2: untwist, torus conversion, ACC += over all waves: item t = (q, j) ----
+        for (int t = tid; t < K1 * M; t += THREADS) {
+            const int q = t >> 8, j = t & (M - 1);  // wave-uniform q (64 consecutive j)
+            const cplx x = cmul(obuf[q * BUF_STRIDE + j], s_utw[j]);
+            uint64_t *poly = acc + q * N;
+            bool o0, o1;
+            uint64_t a0 = torus_add_fast(x.re, poly[j], o0), a1 = torus_add_fast(x.im, poly[j + M], o1);
+            if (__builtin_amdgcn_ballot_w64(!(o0 && o1))) {  // zeros, out-of-range magnitudes (rare)
+                a0 = poly[j] + from_torus_bits(x.re);
+                a1 = poly[j + M] + from_torus_bits(x.im);
+            }
+            poly[j] = a0;
+            poly[j + M] = a1;
+        }
         LPROF(7);
+        lds_sync();
+        LPROF(8);
     }
 #pragma unroll
     for (int i = 0; i < PF; i++) asm volatile("" ::"v"(pf_prev[i]));
 #ifdef TAE_LAT_PROF
     if (blockIdx.x == 0 && lane == 0)
-        printf("latprof wave %2d: dec %llu bar0 %llu fft %llu bar1 %llu mac %llu bar2 %llu inv %llu bar3 %llu\n", jb,
-               (unsigned long long)lprof_[0], (unsigned long long)lprof_[1], (unsigned long long)lprof_[2],
+        printf("latprof wave %2d: dec %llu bar0 %llu fft %llu bar1 %llu mac %llu bar2 %llu inv %llu torus %llu bar3 %llu\n",
+               jb, (unsigned long long)lprof_[0], (unsigned long long)lprof_[1], (unsigned long long)lprof_[2],
                (unsigned long long)lprof_[3], (unsigned long long)lprof_[4], (unsigned long long)lprof_[5],
-               (unsigned long long)lprof_[6], (unsigned long long)lprof_[7]);
+               (unsigned long long)lprof_[6], (unsigned long long)lprof_[7], (unsigned long long)lprof_[8]);
 #endif
     uint64_t *o = out + (size_t)ct * ((K1 - 1) * N + 1);
     for (int t = tid; t < (K1 - 1) * N; t += THREADS) {
