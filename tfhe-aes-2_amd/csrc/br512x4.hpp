@@ -274,6 +274,11 @@ __global__ void __launch_bounds__(THREADS, 1)
 #pragma unroll
         for (int lev = LEV; lev >= 1; lev--) {
             load_level(lev);
+            // the lane's W16 factors, read once for passes A and B (dead before the MAC, so they do
+            // not add to its register peak): 3 of the 11 LDS reads of pass B's LDS-bound phase
+            cplx w16[3];
+#pragma unroll
+            for (int k = 0; k < 3; k++) w16[k] = my_w16[k];
             // pass A (column u): twist, DFT16 over m = r + 4 i, W_M^{u k} -> LDS position u + 16 k
             if (fjob) {
                 cplx v[4];
@@ -287,7 +292,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                     const cplx tw = s_tw[ll + 64 * i];
                     v[i] = {fma(a0, tw.re, -(a1 * tw.im)), fma(a0, tw.im, a1 * tw.re)};
                 }
-                dft16x4<false>(v, my_w16);
+                dft16x4<false>(v, w16);
                 if (lev == LEV) PRIO(1); else PRIO(2);
 #pragma unroll
                 for (int k2 = 0; k2 < 4; k2++) {
@@ -303,7 +308,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                 cplx v[4];
 #pragma unroll
                 for (int i = 0; i < 4; i++) v[i] = jbuf[pidx(16 * u + r + 4 * i)];
-                dft16x4<false>(v, my_w16);
+                dft16x4<false>(v, w16);
                 PRIO(0);
 #pragma unroll
                 for (int k2 = 0; k2 < 4; k2++) jbuf[pidx(16 * u + r + 4 * k2)] = v[k2];
@@ -333,11 +338,14 @@ __global__ void __launch_bounds__(THREADS, 1)
         lds_sync();
         PROF_T(6);
         PRIO(3);
+        cplx w16[3];  // for both inverse passes
+#pragma unroll
+        for (int k = 0; k < 3; k++) w16[k] = my_w16[k];
         if (fjob) {  // pass B^-1 (row u)
             cplx v[4];
 #pragma unroll
             for (int i = 0; i < 4; i++) v[i] = jbuf[pidx(16 * u + r + 4 * i)];
-            dft16x4<true>(v, my_w16);
+            dft16x4<true>(v, w16);
 #pragma unroll
             for (int k2 = 0; k2 < 4; k2++) jbuf[pidx(16 * u + r + 4 * k2)] = v[k2];
         }
@@ -351,7 +359,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                 const int kk = r + 4 * i;
                 v[i] = cmul(jbuf[pidx(u + 16 * kk)], cconj(s_twa[16 * kk + u]));
             }
-            dft16x4<true>(v, my_w16);
+            dft16x4<true>(v, w16);
             uint64_t *poly = acc + jb * ACC_STRIDE;
 #pragma unroll
             for (int k2 = 0; k2 < 4; k2++) {
