@@ -176,6 +176,9 @@ __global__ void __launch_bounds__(THREADS, 1)
         }
         if (fjob) {
             cplx *dst = buf + jb * BUF_STRIDE;
+            cplx w16[3];  // read once for passes A and B
+#pragma unroll
+            for (int k = 0; k < 3; k++) w16[k] = my_w16[k];
             cplx v[4];
 #pragma unroll
             for (int i = 0; i < 4; i++) {
@@ -184,7 +187,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                 const cplx tw = s_tw[ll + 64 * i];
                 v[i] = {fma(a0, tw.re, -(a1 * tw.im)), fma(a0, tw.im, a1 * tw.re)};
             }
-            dft16x4<false>(v, my_w16);
+            dft16x4<false>(v, w16);
 #pragma unroll
             for (int k2 = 0; k2 < 4; k2++) {
                 const int kq = r + 4 * k2;
@@ -194,7 +197,7 @@ __global__ void __launch_bounds__(THREADS, 1)
             // pass B (row u): DFT16 over positions 16 u + r + 4 i, in place
 #pragma unroll
             for (int i = 0; i < 4; i++) v[i] = dst[pidx(16 * u + r + 4 * i)];
-            dft16x4<false>(v, my_w16);
+            dft16x4<false>(v, w16);
 #pragma unroll
             for (int k2 = 0; k2 < 4; k2++) dst[pidx(16 * u + r + 4 * k2)] = v[k2];
         }
@@ -241,10 +244,13 @@ __global__ void __launch_bounds__(THREADS, 1)
         // other waves) ----
         if (jb < K1) {
             cplx *base = obuf + jb * BUF_STRIDE;
+            cplx w16[3];  // read once for both inverse passes
+#pragma unroll
+            for (int k = 0; k < 3; k++) w16[k] = my_w16[k];
             cplx v[4];
 #pragma unroll
             for (int i = 0; i < 4; i++) v[i] = base[pidx(16 * u + r + 4 * i)];
-            dft16x4<true>(v, my_w16);
+            dft16x4<true>(v, w16);
 #pragma unroll
             for (int k2 = 0; k2 < 4; k2++) base[pidx(16 * u + r + 4 * k2)] = v[k2];
             wave_sync();
@@ -253,7 +259,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                 const int kk = r + 4 * i;
                 v[i] = cmul(base[pidx(u + 16 * kk)], cconj(s_twa[16 * kk + u]));
             }
-            dft16x4<true>(v, my_w16);
+            dft16x4<true>(v, w16);
             wave_sync();  // this wave's reads of base precede its writes below (LDS executes in order)
 #pragma unroll
             for (int k2 = 0; k2 < 4; k2++) base[ll + 64 * k2] = v[k2];  // coefficient pair j = ll + 64 k2
