@@ -375,9 +375,11 @@ __global__ void __launch_bounds__(THREADS, 1)
                 poly[j + M] = a1;
             }
         }
-        wave_sync();
+        wave_sync();  // the next step's decomposition reads this wave's ACC writes (in-order LDS)
         PROF_T(8);
+#ifdef TAE_X4_PROF
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
         PROF_T(9);
     }
 #ifdef TAE_X4_PROF
