@@ -24,6 +24,7 @@
 namespace tae {
 namespace br512x4 {
 
+using br512::BUF_STRIDE;
 using br512::K1;
 using br512::lds_sync;
 using br512::M;
@@ -62,17 +63,6 @@ constexpr int C = 3, JOBS = C * K1, THREADS = 1024;
 #endif
 
 constexpr int ACC_STRIDE = N;
-
-// A job's spectrum region holds 256 slots padded in two ways, chosen per hand-off so that both the
-// writer's and the reader's lane groups are bank-conflict-free (MI355X_MICROARCH.md LDS table: b128
-// reads in 4 groups of 16 lanes, b128 writes in 8 groups of 8):
-//   pidx  (q + q / 16): pass B -> MAC reads (with mac_pos), inverse B^-1 -> A^-1;
-//   pidx2 (q + 2 q / 16): pass A -> pass B, MAC store -> inverse B^-1.
-// With pidx alone the pass B and B^-1 reads (a = u, b = r + 4 i) were 2-way in every lane group.
-// Each hand-off is either across a barrier or wave-local with all of a wave's reads of a pass
-// issued before its writes, so the two layouts can share the region.
-constexpr int BUF_STRIDE = 18 * 16;  // cplx
-__device__ __forceinline__ int pidx2(int q) { return q + 2 * (q >> 4); }
 
 __device__ __forceinline__ void swap32(cplx &x, cplx &y) {
     // v_permlane32_swap: lanes 0-31 keep x and receive the partner's (lane + 32) x in y; lanes 32-63
@@ -307,7 +297,7 @@ __global__ void __launch_bounds__(THREADS, 1)
 #pragma unroll
                 for (int k2 = 0; k2 < 4; k2++) {
                     const int k = r + 4 * k2;
-                    jbuf[pidx2(u + 16 * k)] = cmul(v[k2], s_twa[16 * k + u]);
+                    jbuf[pidx(u + 16 * k)] = cmul(v[k2], s_twa[16 * k + u]);
                 }
             }
             wave_sync();
@@ -317,7 +307,7 @@ __global__ void __launch_bounds__(THREADS, 1)
             if (fjob) {
                 cplx v[4];
 #pragma unroll
-                for (int i = 0; i < 4; i++) v[i] = jbuf[pidx2(16 * u + r + 4 * i)];
+                for (int i = 0; i < 4; i++) v[i] = jbuf[pidx(16 * u + r + 4 * i)];
                 dft16x4<false>(v, w16);
                 PRIO(0);
 #pragma unroll
@@ -340,10 +330,10 @@ __global__ void __launch_bounds__(THREADS, 1)
         }
         // ---- inverse FFT of the MAC results, accumulated into ACC ----
         switch (grp) {
-        case 0: mac_store<0>(buf, pidx2(pos), accr); break;
-        case 1: mac_store<1>(buf, pidx2(pos), accr); break;
-        case 2: mac_store<2>(buf, pidx2(pos), accr); break;
-        default: mac_store<3>(buf, pidx2(pos), accr); break;
+        case 0: mac_store<0>(buf, pidx(pos), accr); break;
+        case 1: mac_store<1>(buf, pidx(pos), accr); break;
+        case 2: mac_store<2>(buf, pidx(pos), accr); break;
+        default: mac_store<3>(buf, pidx(pos), accr); break;
         }
         lds_sync();
         PROF_T(6);
@@ -354,7 +344,7 @@ __global__ void __launch_bounds__(THREADS, 1)
         if (fjob) {  // pass B^-1 (row u)
             cplx v[4];
 #pragma unroll
-            for (int i = 0; i < 4; i++) v[i] = jbuf[pidx2(16 * u + r + 4 * i)];
+            for (int i = 0; i < 4; i++) v[i] = jbuf[pidx(16 * u + r + 4 * i)];
             dft16x4<true>(v, w16);
 #pragma unroll
             for (int k2 = 0; k2 < 4; k2++) jbuf[pidx(16 * u + r + 4 * k2)] = v[k2];
