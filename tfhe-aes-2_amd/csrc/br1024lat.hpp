@@ -9,7 +9,8 @@
 //        the MAC threads' GGSW rows of the pass's first level are loaded meanwhile
 //     M  MAC chains (q, Fourier position): 1536 on 1024 threads (threads < 512 run q = 2 as well),
 //        each chain p ascending with the oracle's fma order, the pass's levels descending
-//   S  MAC results -> LDS;  I  inverse FFT of the 3 outputs (waves 0-2), untwist, torus, ACC +=
+//   S  MAC results -> LDS;  I  inverse FFT of the 3 outputs (waves 0-2);  I2 untwist, torus, ACC +=
+//      over all 16 waves
 // Every output keeps br1024's (and the oracle's) operation order: results are bit-identical to it.
 // LDS (155 KiB): ACC [3][1024] u64, spectra [3 LP][576] cplx, twist / W_512 / untwist and the pass-0/1
 // twiddle tables, digits [LEV][3][512] (int8 pairs).
@@ -277,20 +278,25 @@ __global__ void __launch_bounds__(THREADS, 1)
                 v[kk] = csel(t != 0, tv, y);
             }
             dft8<true>(v, w81, w83);
-            uint64_t *poly = acc + jb * N;
+            wave_sync();  // this wave's reads of Y precede its writes below (LDS executes in order)
 #pragma unroll
-            for (int m = 0; m < 8; m++) {
-                const int j = t + 64 * m;
-                const cplx tt = cmul(v[m], s_utw[j]);
-                bool o0, o1;
-                uint64_t a0 = torus_add_fast(tt.re, poly[j], o0), a1 = torus_add_fast(tt.im, poly[j + M], o1);
-                if (__builtin_amdgcn_ballot_w64(!(o0 && o1))) {  // zeros, out-of-range magnitudes (rare)
-                    a0 = poly[j] + from_torus_bits(tt.re);
-                    a1 = poly[j + M] + from_torus_bits(tt.im);
-                }
-                poly[j] = a0;
-                poly[j + M] = a1;
+            for (int m = 0; m < 8; m++) Y[t + 64 * m] = v[m];  // coefficient pair j = t + 64 m
+        }
+        br512::lds_sync();
+        // ---- I2: untwist, from_torus, ACC += over all 16 waves (in I they were a fifth of the three
+        // inverse waves' VALU work): item i = (q, j), wave-uniform q ----
+        for (int i = tid; i < K1 * M; i += THREADS) {
+            const int q = i >> 9, j = i & (M - 1);
+            const cplx tt = cmul(buf[q * BUF_STRIDE + j], s_utw[j]);
+            uint64_t *poly = acc + q * N;
+            bool o0, o1;
+            uint64_t a0 = torus_add_fast(tt.re, poly[j], o0), a1 = torus_add_fast(tt.im, poly[j + M], o1);
+            if (__builtin_amdgcn_ballot_w64(!(o0 && o1))) {  // zeros, out-of-range magnitudes (rare)
+                a0 = poly[j] + from_torus_bits(tt.re);
+                a1 = poly[j + M] + from_torus_bits(tt.im);
             }
+            poly[j] = a0;
+            poly[j + M] = a1;
         }
         QPROF(5);
         br512::lds_sync();  // the next decomposition reads every polynomial
