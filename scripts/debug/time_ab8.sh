@@ -4,6 +4,6 @@
 cd "$(dirname "$0")/../.."
 for pass in 1 2; do
   for lib in tfhe-aes-2_amd/dbg/*.so; do
-    TAE_PBS_B=256 TAE_LIB_PATH=$PWD/$lib timeout -k 10 200 python scripts/debug/time_pbs8.py 2>&1 | tail -1 || exit 1
+    TAE_PBS_B=${PBS_B:-256} TAE_LIB_PATH=$PWD/$lib timeout -k 10 200 python scripts/debug/time_pbs8.py 2>&1 | tail -1 || exit 1
   done
 done
