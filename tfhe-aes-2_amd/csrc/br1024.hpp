@@ -169,6 +169,16 @@ __global__ void __launch_bounds__(THREADS, 1)
             w1r[kk - 1] = s_w1[(kk - 1) * 8 + (tid & 7)];
         }
     }
+    // likewise the lane's eight twist factors of pass 0, for the 8-bit model's shapes where it was
+    // measured (62.2 vs 64.1 ms for the CBS launch, same box, although its PBS instantiation then
+    // spills 18 VGPRs outside the FFT passes; the lvl_1/4/256 shapes would spill more, unmeasured)
+    constexpr bool TWREG = WREG && BLOG <= 7;
+    cplx twr[8];
+    if constexpr (TWREG) {
+#pragma unroll
+        for (int m = 0; m < 8; m++) twr[m] = s_tw[(tid & 63) + 64 * m];
+    }
+#define TW_AT(m) (TWREG ? twr[m] : s_tw[tt + 64 * (m)])
 #define W0_AT(kk) (WREG ? w0r[(kk) - 1] : s_w0[((kk) - 1) * 64 + tt])
 #define W1_AT(kk) (WREG ? w1r[(kk) - 1] : s_w1[((kk) - 1) * 8 + uu])
 
@@ -267,7 +277,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                         a0 = br512::lo16(dw);
                         a1 = br512::hi16(dw);
                     }
-                    const cplx tw = s_tw[tt + 64 * m];
+                    const cplx tw = TW_AT(m);
                     v[m] = {fma(a0, tw.re, -(a1 * tw.im)), fma(a0, tw.im, a1 * tw.re)};
                 }
                 dft8<false>(v, w81, w83);
@@ -415,6 +425,7 @@ __global__ void __launch_bounds__(THREADS, 1)
 
 #undef W0_AT
 #undef W1_AT
+#undef TW_AT
 
 inline size_t lds_bytes(int C, int LP = 1) {
     return (size_t)C * K1 * ACC_STRIDE * 8 + (size_t)C * K1 * LP * BUF_STRIDE * 16 + 3 * (size_t)M * 16 +
