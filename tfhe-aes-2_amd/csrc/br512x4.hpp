@@ -240,7 +240,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                     }
                 }
         };
-        PRIO(2);
+        PRIO(3);  // (2 here and a step-down in level 3's pass A: +0.5-0.9% time, same box)
         // ---- rotated difference + decomposition of coefficients j = u + 16 r + 64 i (+ M) ----
         int ll = lane;
         asm volatile("" : "+v"(ll));
@@ -293,7 +293,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                     v[i] = {fma(a0, tw.re, -(a1 * tw.im)), fma(a0, tw.im, a1 * tw.re)};
                 }
                 dft16x4<false>(v, w16);
-                if (lev == LEV) PRIO(1); else PRIO(2);
+                PRIO(2);
 #pragma unroll
                 for (int k2 = 0; k2 < 4; k2++) {
                     const int k = r + 4 * k2;
