@@ -293,7 +293,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                     v[i] = {fma(a0, tw.re, -(a1 * tw.im)), fma(a0, tw.im, a1 * tw.re)};
                 }
                 dft16x4<false>(v, w16);
-                PRIO(2);
+                if (lev == LEV) PRIO(2);  // levels below the first keep 3 through pass A (-0.9%, same box)
 #pragma unroll
                 for (int k2 = 0; k2 < 4; k2++) {
                     const int k = r + 4 * k2;
