@@ -53,6 +53,44 @@ def test_full_batch_128_blocks_two_rounds(gpu_context, oracle_keys, client, read
         assert np.array_equal(out[b], ref), b
 
 
+def test_configs3_rank7_of_8_shard(oracle_keys, product_raw, client):
+    """BASELINE configs[3] (1024 blocks over 8 GPUs) as its LAST rank runs it, on this one GPU: exactly
+    what bench.py does on rank 7 of world 8 with 128 blocks per GPU (main.rs:108-115 counters, sharded
+    as main.rs:148-152 runs them): counters 897..1024 from D.counter_blocks_for_rank, encryption indices
+    from D.encrypt_start_index(7, 128), a context built from torch-resident server keys with
+    TAE_MEM_DEVICE (the RCCL broadcast's destination buffers), the round key resident on the device and
+    encrypt_blocks_device.  2 rounds (reduced-round semantics); all 128 blocks decrypt to plain AES, and
+    blocks 0, 126 (first past the br512x4 / br512lat split) and 127 equal the oracle word for word."""
+    torch = pytest.importorskip("torch")
+    from tfhe_aes import distributed as D
+    rank, world, nb, rounds = 7, 8, 128, 2
+    g_key = bytes.fromhex("76b8e0ada0f13d90405d6ae55386bd28")  # README key / iv (main.rs:108-115)
+    g_iv = bytes.fromhex("bdd219b8a08ded1a")
+    blocks = D.counter_blocks_for_rank(g_iv, rank, world, nb)
+    assert int.from_bytes(blocks[0][8:], "big") == 897 and int.from_bytes(blocks[-1][8:], "big") == 1024
+    _, keys = product_raw
+    dev = [torch.from_numpy(k.view(np.int64)).to("cuda:0") for k in keys]
+    ctx_d = tfhe_aes.context_from_raw(tfhe_aes.PARAMS_SQRD_LVL_64, [t.data_ptr() for t in dev], device=0,
+                                      mem=N.TAE_MEM_DEVICE)
+    ek = b"".join(aes_128.key_schedule_plain(g_key))
+    rk = client.encrypt_bits_raw([b for byte in ek for b in aes_128.u8_to_bits(byte)], start_index=600_000)
+    cts = client.encrypt_bits_raw(aes_128.blocks_to_bits(blocks),
+                                  start_index=D.encrypt_start_index(rank, nb)).reshape(nb, 128, BIG)
+    d_rk = torch.from_numpy(rk.view(np.int64)).to("cuda:0")
+    d_in = torch.from_numpy(cts.view(np.int64)).to("cuda:0")
+    d_out = torch.full_like(d_in, -1)
+    torch.cuda.synchronize()
+    E.encrypt_blocks_device(ctx_d, d_rk.data_ptr(), d_in.data_ptr(), nb, rounds, d_out.data_ptr())
+    ctx_d.synchronize()
+    out = d_out.cpu().numpy().view(np.uint64)
+    got = aes_128.bits_to_blocks(client.decrypt_bits_raw(out))
+    assert got == aes_128.expand_key_and_encrypt_blocks(g_key, blocks, rounds)
+    for b in (0, 126, nb - 1):
+        ref = oracle_keys.aes_encrypt_block(rk, cts[b], rounds, threads=16)
+        assert np.array_equal(out[b], ref), b
+    del ctx_d  # the context borrows the key buffers: free it first
+
+
 def test_device_key_context_matches_host_context(gpu_context, product_raw, client, readme_setup):
     torch = pytest.importorskip("torch")
     _, keys = product_raw

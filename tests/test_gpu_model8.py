@@ -81,11 +81,13 @@ def test_pbs8_kernel_variants_bit_exact(product_raw8, oracle_keys8, client8, lat
 def test_pfks8_bit_exact(gpu_context8, oracle_keys8, client8):
     small = client8.encrypt_bits_raw([1, 0], start_index=300)
     big = np.stack([oracle_keys8.homomorphic_shift_boolean(small[i], 2) for i in range(2)])
-    out = np.zeros((2, 4, 3, 3 * 1024), dtype=np.uint64)  # [B][cbs_l][k+1][(k+1)N]
+    out = np.full((2, 4, 3, 3 * 1024), 0x5A5A, dtype=np.uint64)  # [B][cbs_l][k+1][(k+1)N], poisoned
     _stage(N.lib().tae_stage_pfks_ggsw, gpu_context8._h, _vp(big), 2, 2, _vp(out), N.TAE_MEM_HOST)
     for i in range(2):
         for q in range(3):
             assert np.array_equal(out[i, 1, q], oracle_keys8.pfks(q, big[i])), (i, q)
+    # the stage writes only level 2's rows; the host path hands back zeros for the other levels
+    assert not out[:, [0, 2, 3]].any()
 
 
 @pytest.mark.parametrize("layout", ["k", "rows"])

@@ -82,3 +82,28 @@ def test_save_rejects_mismatched_params(product_raw, tmp_path):
     with pytest.raises(tfhe_aes.TaeError):
         tfhe_aes.save_keys(tmp_path / "x.taekey", tfhe_aes.PARAMS_WOPPBS_8BIT, ck)
     assert not os.path.exists(tmp_path / "y.taekey")
+
+
+def _rehash(body):
+    """The file checksum (keyio.cpp Hash): word-wise FNV-1a over a multiple of 8 bytes."""
+    h = 0xcbf29ce484222325
+    for i in range(0, len(body), 8):
+        h = ((h ^ int.from_bytes(body[i:i + 8], "little")) * 0x100000001b3) & (2**64 - 1)
+    return body + h.to_bytes(8, "little")
+
+
+def test_legacy_v01_client_key_is_rejected(product_raw, tmp_path):
+    """A TAEKEY01 client counter reserved the LOW indices its tae_encrypt ciphertexts used, which explicit
+    raw ranges may now reach (tae_encrypt draws from 2^63 + counter): such a file must not load."""
+    ck, _ = product_raw
+    path = tmp_path / "client.taekey"
+    tfhe_aes.save_keys(path, tfhe_aes.PARAMS_SQRD_LVL_64, ck)
+    data = open(path, "rb").read()
+    assert data[:8] == b"TAEKEY02" and len(data) == 64
+    legacy = tmp_path / "legacy.taekey"
+    open(legacy, "wb").write(_rehash(b"TAEKEY01" + data[8:-8]))
+    with pytest.raises(tfhe_aes.TaeError) as e:
+        tfhe_aes.load_keys(legacy)
+    assert e.value.code == 5 and "legacy" in str(e.value)
+    open(tmp_path / "v02.taekey", "wb").write(_rehash(data[:-8]))  # the re-hash itself is right
+    assert tfhe_aes.load_keys(tmp_path / "v02.taekey")[0] is not None

@@ -117,8 +117,11 @@ void staged(tae_context const *ctx, const TI *in, size_t in_bytes, TO *out, size
         throw tae::HipError{"hipMalloc"};
     }
     try {
-        // everything on the engine stream, in order (the kernels overwrite every output word)
+        // everything on the engine stream, in order.  The output is cleared first: not every stage
+        // writes every word (tae_stage_pfks_ggsw fills only the rows of the requested level), and the
+        // caller must get zeros there, not uninitialized device memory.
         tae::hip_check(hipMemcpyAsync(di, in, in_bytes, hipMemcpyHostToDevice, e.stream()), "upload");
+        tae::hip_check(hipMemsetAsync(dout, 0, out_bytes, e.stream()), "clear output");
         call(static_cast<const TI *>(di), static_cast<TO *>(dout));
         tae::hip_check(hipMemcpyAsync(out, dout, out_bytes, hipMemcpyDeviceToHost, e.stream()), "download");
         e.synchronize();
@@ -430,7 +433,7 @@ int tae_generate_multivariate_luts(int poly_size, int input_bits, int output_bit
         require(f_values && out, "null");
         require(poly_size >= 2 && (poly_size & (poly_size - 1)) == 0 && poly_size <= (1 << 16),
                 "polynomial size must be a power of two");
-        require(input_bits >= 1 && input_bits <= 24 && output_bits >= 1 && output_bits <= 64, "bit counts out of range");
+        require(input_bits >= 1 && input_bits <= 16 && output_bits >= 1 && output_bits <= 64, "bit counts out of range");
         require(out_len == tae::lut_small_len(poly_size, input_bits) * (size_t)output_bits, "length mismatch");
         tae::generate_lut(poly_size, input_bits, output_bits, f_values, out);
     });
@@ -446,8 +449,9 @@ int tae_xor_batch(const tae_context *ctx, uint64_t *lhs, const uint64_t *rhs, si
             // BitXorAssign's noise rule (shortint_woppbs_1bit.rs:134-142, NoiseLevelWithComponents::add
             // + MaxNoiseLevel::validate): squared noise levels add and must stay <= max_noise_level^2
             for (size_t i = 0; i < count; i++) {
-                const uint64_t s = lhs_noise_sq[i] + rhs_noise_sq[i];
-                if (s > max_sq)
+                const uint64_t l = lhs_noise_sq[i], r = rhs_noise_sq[i];
+                const uint64_t s = l + r;
+                if (l > max_sq || r > max_sq - l)  // no wrap-around: l + r <= max_sq exactly
                     throw tae::ModelError{TAE_E_NOISE, "NoiseTooBig: noise level squared " + std::to_string(s) +
                                                            " above " + std::to_string(max_sq) + " at element " +
                                                            std::to_string(i)};

@@ -2,7 +2,7 @@
 // SURVEY.md §8f-2); a service needs to persist a client key and ship server keys to evaluation
 // nodes.  One self-describing little-endian file holds either or both:
 //
-//   "TAEKEY01"                     8-byte magic + format version
+//   "TAEKEY02"                     8-byte magic + format version
 //   u32 param_set, u32 flags       flags: 1 = client key, 2 = server keys
 //   [flags & 1] u8 seed[32], u64 next_index
 //                                  the client key is re-derived from its seed (generate_client_key,
@@ -11,6 +11,11 @@
 //   [flags & 2] u64 ksk_len, bsk_len, pfpksk_len, then the three standard-domain u64 arrays
 //                                  (the lengths must equal tae_server_key_sizes(param_set))
 //   u64 checksum                   word-wise FNV-1a over every preceding byte
+//
+// Version 01 (round 2 and earlier) stored a client counter whose tae_encrypt ciphertexts used the LOW
+// indices [0, next_index); tae_encrypt now draws from 2^63 + next_index and explicit raw ranges may use
+// anything below 2^63, so a reloaded 01 client key could reuse those streams.  01 files are therefore
+// still read for their server keys, but a 01 file holding a client key is rejected (re-save it).
 //
 // A file is rejected (TAE_E_ARG) on a bad magic, unknown flags or parameter set, a size mismatch,
 // truncation or a checksum mismatch; nothing is returned from a rejected file.
@@ -26,7 +31,8 @@
 namespace tae {
 namespace keyio {
 
-constexpr char kMagic[8] = {'T', 'A', 'E', 'K', 'E', 'Y', '0', '1'};
+constexpr char kMagic[8] = {'T', 'A', 'E', 'K', 'E', 'Y', '0', '2'};
+constexpr char kMagicV1[8] = {'T', 'A', 'E', 'K', 'E', 'Y', '0', '1'};
 constexpr uint32_t kClient = 1, kServer = 2;
 
 struct Hash {
@@ -121,12 +127,15 @@ void load(const char *path, int *param_set, uint32_t *flags, ClientKey *ck, uint
     Hash h;
     char magic[8];
     get(f, h, magic, 8);
-    if (std::memcmp(magic, kMagic, 8) != 0) bad("not a TAEKEY01 file");
+    const bool v1 = std::memcmp(magic, kMagicV1, 8) == 0;
+    if (!v1 && std::memcmp(magic, kMagic, 8) != 0) bad("not a TAEKEY02 file");
     uint32_t hdr[2];
     get(f, h, hdr, sizeof(hdr));
     Params p;
     if (!get_params((int)hdr[0], p)) bad("unknown parameter set");
     if (hdr[1] == 0 || (hdr[1] & ~(kClient | kServer))) bad("unknown flags");
+    if (v1 && (hdr[1] & kClient))
+        bad("legacy TAEKEY01 client key: its counter does not reserve the indices it used; re-save the key");
     *param_set = (int)hdr[0];
     *flags = hdr[1];
     const bool header_only = !ck && !ksk && !bsk && !pfpksk;

@@ -635,6 +635,7 @@ void Context::aes_key_schedule_raw(const uint64_t *key, uint64_t *expanded, bool
     const size_t L = bit_len();
     std::vector<uint64_t> hk(128 * L);
     if (device_mem) {
+        std::lock_guard<std::mutex> g(mu_);  // the engine (and its device) is shared: same lock as every entry
         engine_->order_after_caller();
         hip_check(hipMemcpy(hk.data(), key, hk.size() * 8, hipMemcpyDeviceToHost), "download key");
     } else {

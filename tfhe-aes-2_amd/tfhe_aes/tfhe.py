@@ -383,7 +383,7 @@ def context_from_raw(param_set: int, keys, device: int = 0, mem: int = N.TAE_MEM
 
 # ---- on-disk keys (include/tfhe_aes_gpu.h tae_keys_*; format in csrc/keyio.cpp) ----
 def save_keys(path, param_set: int, client_key: "ClientKey | None" = None, server_keys=None) -> None:
-    """Write a TAEKEY01 file with the client key (seed + encryption counter) and/or the raw server
+    """Write a TAEKEY02 file with the client key (seed + encryption counter) and/or the raw server
     keys (ksk, bsk, pfpksk) as returned by generate_keys_raw."""
     ptrs = [None, None, None]
     if server_keys is not None:
@@ -400,7 +400,7 @@ def key_file_info(path) -> tuple:
 
 
 def load_keys(path, client: bool = True, server: bool = True):
-    """(client_key or None, (ksk, bsk, pfpksk) or None) from a TAEKEY01 file; the checksum is
+    """(client_key or None, (ksk, bsk, pfpksk) or None) from a TAEKEY02 file; the checksum is
     verified before anything is returned."""
     param_set, has_ck, has_sk = key_file_info(path)
     client, server = client and has_ck, server and has_sk
