@@ -70,7 +70,7 @@ def main():
                     help="with --model 1bit: also time BASELINE config #5 (8-bit model) on a bounded batch "
                          "(--model8-blocks blocks, one step) and report it beside the headline line; auto = on "
                          "at world size 1")
-    ap.add_argument("--model8-blocks", type=int, default=16)
+    ap.add_argument("--model8-blocks", type=int, default=64)
     ap.add_argument("--host-buffers", choices=["auto", "on", "off"], default="auto",
                     help="one extra step with host arrays (PCIe-inclusive rate); auto = on at world 1")
     args = ap.parse_args()
@@ -253,7 +253,7 @@ def main():
     stage_tflops = flop_launch / (pbs_ms * 1e-3) / 1e12 if pbs_ms > 0 else None
     # HBM traffic per launch of the same kernel from the committed PMC pass (scripts/bench_profile.sh
     # -> scripts/prof_summary.py: 2 x FETCH_SIZE + WRITE_SIZE), valid only for the same batch shape.
-    traffic, traffic_src, traffic_dram = None, None, None
+    traffic, traffic_src = None, None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if os.path.exists(pmc_path):
         with open(pmc_path) as fh:
@@ -261,12 +261,13 @@ def main():
         ent = pm.get("kernels", {}).get(PBS_KERNEL, {})
         if pm.get("blocks_per_gpu") == nb and "hbm_bytes_per_launch" in ent:
             traffic, traffic_src = ent["hbm_bytes_per_launch"], pm.get("source")
-            traffic_dram = ent.get("hbm_dram_bytes_per_launch")
     # The batched blind rotation is bound by the FP64 vector ALU (>= 10 flop/B at any
     # batch; no MFMA on this path): peak = the dense FP64 vector rate, HBM figures ride along.
     roofline = {"bound": "fp64_valu", "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": (tflops / FP64_PEAK_TFLOPS) if tflops else None, "traffic": traffic,
-                "traffic_unit": "bytes/launch", "traffic_source": traffic_src, "traffic_dram": traffic_dram,
+                "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
+                "traffic_note": "L2-miss bytes (2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md): they include "
+                                "Infinity-Cache hits, and no counter here separates the bytes that reached HBM",
                 "kernel": PBS_KERNEL + " (homomorphic_shift_boolean blind rotation)", "avg_launch_ms": k_ms,
                 "ciphertexts_per_launch": main_cts if main_ms > 0 else nb * 16 * 8,
                 "algorithmic_flop_per_launch": k_flop,

@@ -70,6 +70,18 @@ __device__ __forceinline__ void body(double *d, unsigned *u, unsigned long long 
 #define F(i) asm volatile("v_fma_f64 %0, %0, %1, %1" : "+v"(d[(i) & 1]) : "v"(d[2]));
         REP8(F) REP8(F)
 #undef F
+    } else if constexpr (CLS == 16) {  // v_cndmask_b32 with a DPP quad_perm source (the 2-lane exchange)
+#define F(i) asm volatile("v_cndmask_b32_dpp %0, %1, %0, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(u[i]) : "v"(u[(i + 3) & 7]));
+        REP8(F) REP8(F)
+#undef F
+    } else if constexpr (CLS == 17) {  // v_permlane16_swap
+#define F(i) { const auto r_ = __builtin_amdgcn_permlane16_swap(u[i], u[(i + 4) & 7], false, false); u[i] = r_[0]; u[(i + 4) & 7] = r_[1]; }
+        REP8(F) REP8(F)
+#undef F
+    } else if constexpr (CLS == 18) {  // v_mul_f64
+#define F(i) asm volatile("v_mul_f64 %0, %0, %1" : "+v"(d[i]) : "v"(d[(i + 1) & 7]));
+        REP8(F) REP8(F)
+#undef F
     } else if constexpr (CLS == 11) {  // v_pk_fma_f32
 #define F(i) asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(q[i]) : "v"(q[(i + 1) & 7]), "v"(q[(i + 2) & 7]));
         REP8(F) REP8(F)
@@ -118,7 +130,8 @@ float run(double *d, int blocks, int iters) {
 
 static const char *names[] = {"v_fma_f64", "v_add_u32", "v_lshlrev_b64", "v_permlane32_swap", "v_add_f64",
                               "v_pk_add_u16", "v_cvt_f64_i32", "v_mul_lo_u32", "v_lshl_add_u64", "v_cndmask_b32",
-                              "v_mov_b32", "v_pk_fma_f32", "fma_f64 dep1", "v_mov_dpp", "cndmask_sgpr", "fma_f64 dep2"};
+                              "v_mov_b32", "v_pk_fma_f32", "fma_f64 dep1", "v_mov_dpp", "cndmask_sgpr", "fma_f64 dep2",
+                              "v_cndmask_dpp", "v_permlane16_swap", "v_mul_f64"};
 
 template <int A, int B, int T = 1024>
 void report(double *d, int blocks, int iters, double ghz) {
@@ -175,5 +188,10 @@ int main() {
     report<14, 14, 1024>(d, cus, iters, ghz);
     report<15, 15, 1024>(d, cus, iters, ghz);
     report<15, 15, 256>(d, cus, iters, ghz);
+    report<16, 16, 1024>(d, cus, iters, ghz);
+    report<17, 17, 1024>(d, cus, iters, ghz);
+    report<18, 18, 1024>(d, cus, iters, ghz);
+    report<0, 16, 1024>(d, cus, iters, ghz);
+    report<0, 17, 1024>(d, cus, iters, ghz);
     return 0;
 }

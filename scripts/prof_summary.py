@@ -68,21 +68,16 @@ def main():
             cs["hbm_bytes_per_launch"] = fetch + write
             cs["hbm_read_bytes_per_launch_corrected"] = fetch
             cs["hbm_write_bytes_per_launch"] = write
-            # L2 misses (FETCH_SIZE) include Infinity-Cache hits (MI355X_MICROARCH.md HBM section); the
-            # DRAM share of the L2's read requests (TCC_EA0_RDREQ_DRAM / TCC_EA0_RDREQ, own pass) splits
-            # them into on-die and HBM reads
-            if "TCC_EA0_RDREQ_DRAM" in cs and cs.get("TCC_EA0_RDREQ", {}).get("avg_per_dispatch"):
-                share = cs["TCC_EA0_RDREQ_DRAM"]["avg_per_dispatch"] / cs["TCC_EA0_RDREQ"]["avg_per_dispatch"]
-                cs["dram_read_share"] = share
-                cs["hbm_dram_bytes_per_launch"] = fetch * share + write
+            # L2 misses (FETCH_SIZE) include Infinity-Cache hits (MI355X_MICROARCH.md HBM section).
+            # TCC_EA0_RDREQ_DRAM reads equal TCC_EA0_RDREQ for every large kernel here, so it does not
+            # separate Infinity-Cache hits either: no DRAM-only figure is derived from it.
     with open(os.path.join(dst, "pmc.json"), "w") as fh:
         json.dump(pmc, fh, indent=1, sort_keys=True)
     blocks = int(sys.argv[2]) if len(sys.argv) > 2 else None
     latest = {"blocks_per_gpu": blocks,
               "source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE passes of bench.py --steps 1 "
                         "--key-schedule plain (scripts/bench_profile.sh); bytes = 2 x FETCH_SIZE + WRITE_SIZE "
-                        "(L2 misses incl. Infinity-Cache hits); hbm_dram_bytes_per_launch scales the reads by "
-                        "TCC_EA0_RDREQ_DRAM / TCC_EA0_RDREQ",
+                        "(L2 misses incl. Infinity-Cache hits; no counter separates the bytes that reached HBM)",
               "kernels": {k: {c: (v["avg_per_dispatch"] if isinstance(v, dict) else v) for c, v in cs.items()}
                           for k, cs in pmc.items()}}
     with open(os.path.join(dst, "pmc_latest.json"), "w") as fh:

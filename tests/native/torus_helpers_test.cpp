@@ -64,6 +64,21 @@ static void check_dec(uint64_t x, int B) {
     }
 }
 
+// level-by-level digit chain == the oracle's digits, finest level first
+template <int LEV, int B>
+static void check_chain(uint64_t x) {
+    int64_t r[LEV];
+    or_decompose(x, B, LEV, r);
+    uint32_t st;
+    int32_t got = tae::digit_first<LEV, B>(x, st);
+    for (int l = LEV - 1; l >= 0; l--) {
+        if (l < LEV - 1) got = tae::digit_next<B>(st);
+        if (got != r[l] && fails++ < 10)
+            printf("digit chain(%016llx, B=%d, L=%d) level %d: got %d want %lld\n", (unsigned long long)x, B, LEV, l + 1,
+                   got, (long long)r[l]);
+    }
+}
+
 // packed two-coefficient decomposition == decompose16 on each half
 template <int LEV, int B>
 static void check_decp(uint64_t x0, uint64_t x1) {
@@ -118,6 +133,10 @@ int main(int argc, char **argv) {
         check_dect<4, 6>(x);
         check_dect<3, 12>(x);
         check_dect<4, 9>(x);
+        check_chain<3, 12>(x);
+        check_chain<1, 13>(x);
+        check_chain<4, 6>(x);
+        check_chain<2, 15>(x);
     }
     for (long i = 0; i < n; i++) {
         uint64_t x = rng();
@@ -132,6 +151,11 @@ int main(int argc, char **argv) {
         check_dect<4, 6>(x);
         check_dect<3, 12>(x);
         check_dect<4, 9>(x);
+        check_chain<3, 12>(x);
+        check_chain<1, 13>(x);
+        check_chain<4, 6>(x);
+        check_chain<2, 15>(x);
+        check_chain<3, 9>(x);
         const uint64_t y = (i & 2) ? rng() : (x ^ (rng() & 0xFFFFFFFull));
         check_decp<3, 12>(x, y);
         check_decp<1, 13>(x, y);

@@ -299,6 +299,32 @@ __host__ __device__ __forceinline__ void decompose16p(uint64_t x0, uint64_t x1, 
     }
 }
 
+// The same digits one level at a time, least significant level first, as signed 32-bit values (what
+// v_cvt_f64_i32 takes): digit_first returns the digit of the finest level (LEV) of x and leaves the
+// 32-bit state of the fields above it (carry included) in st; each digit_next returns the digit of the
+// next coarser level and advances st.  Unpacked 32-bit ops cost half a v_pk_*_u16 op each on gfx950,
+// and the state (one register per coefficient) replaces the packed digits of every level.
+template <int LEV, int B>
+__host__ __device__ __forceinline__ int32_t digit_first(uint64_t x, uint32_t &st) {
+    static_assert(B * (LEV - 1) < 32 && B >= 2 && B <= 16, "digit_first shape");
+    constexpr int nrb = 64 - B * LEV;
+    const uint64_t X = x + (1ull << (nrb - 1));
+    const uint32_t res = (uint32_t)(X >> nrb) & ((1u << B) - 1);
+    if constexpr (nrb + B >= 64) st = 0u;
+    else st = (uint32_t)(X >> (nrb + B));
+    const uint32_t c = (((res - 1) | st) & res) >> (B - 1);
+    st += c;
+    return (int32_t)res - (int32_t)(c << B);
+}
+template <int B>
+__host__ __device__ __forceinline__ int32_t digit_next(uint32_t &st) {
+    const uint32_t res = st & ((1u << B) - 1);
+    st >>= B;
+    const uint32_t c = (((res - 1) | st) & res) >> (B - 1);
+    st += c;
+    return (int32_t)res - (int32_t)(c << B);
+}
+
 // pbs_modulus_switch: round(x * 2N / 2^64) in [0, 2N]
 __device__ __forceinline__ int mod_switch(uint64_t x, int logN) {
     uint64_t o = x >> (64 - logN - 2);
