@@ -16,6 +16,7 @@ _SO = os.path.join(_HERE, "build", "liboracle.so")
 
 PARAMS_SQRD_LVL_1, PARAMS_SQRD_LVL_4, PARAMS_SQRD_LVL_64, PARAMS_SQRD_LVL_256 = 0, 1, 2, 3
 PARAMS_WOPPBS_8BIT = 4  # shortint_woppbs_8bit.rs:39-86
+PARAMS_SHORTINT_1BIT = 5  # shortint_1bit.rs:62-83
 
 
 def build() -> str:
@@ -27,7 +28,7 @@ class _Params(C.Structure):
     _fields_ = [(n, C.c_int) for n in
                 ("n", "k", "N", "pbs_l", "pbs_b", "ks_l", "ks_b", "cbs_l", "cbs_b", "pfks_l", "pfks_b")] + [
         ("lwe_std", C.c_double), ("glwe_std", C.c_double), ("pfks_std", C.c_double),
-        ("max_noise_sq", C.c_uint64)]
+        ("max_noise_sq", C.c_uint64), ("model", C.c_int)]
 
 
 class _ClientKey(C.Structure):
@@ -121,6 +122,15 @@ def lib():
         L.or_aes8_encrypt_block.argtypes = [C.c_void_p, u64p, u64p, C.c_int, C.c_int, u64p]
         L.or_gf_256_mul_quirk.argtypes = [C.c_uint8, C.c_uint8]
         L.or_gf_256_mul_quirk.restype = C.c_uint8
+        L.or_s1_encrypt.argtypes = [C.c_void_p, C.c_char_p, C.c_uint64, C.c_uint64, u64p]
+        L.or_s1_decrypt.argtypes = [C.c_void_p, u64p]
+        L.or_s1_decrypt.restype = C.c_uint64
+        L.or_s1_tv_from_fn.argtypes = [C.c_int, C.c_int, C.c_uint64, C.c_uint64, u64p]
+        L.or_s1_pks.argtypes = [C.c_void_p, u64p, u64p]
+        L.or_s1_pack.argtypes = [C.c_void_p, u64p, C.c_int, u64p]
+        L.or_s1_tv_from_cts.argtypes = [C.c_void_p, u64p, u64p, u64p]
+        L.or_s1_bootstrap.argtypes = [C.c_void_p, u64p, u64p, u64p]
+        L.or_s1_multivariate.argtypes = [C.c_void_p, u64p, C.c_int, u64p, u64p]
         _lib = L
     return _lib
 
@@ -319,6 +329,67 @@ class Keys:
         out = np.zeros((128, self.p["n"] + 1), dtype=np.uint64)
         lib().or_aes8_encrypt_block(self.sk, _p64(np.ascontiguousarray(rk, dtype=np.uint64)),
                                     _p64(np.ascontiguousarray(block, dtype=np.uint64)), rounds, threads, _p64(out))
+        return out
+
+
+class S1Keys(Keys):
+    """shortint_1bit model (param id 5, src/tfhe/shortint_1bit.rs): bits are shortint ciphertexts under the
+    SMALL key [n+1], test vectors are GLWEs [(k+1)N]."""
+
+    def __init__(self, seed: bytes, threads: int = 8, raw=None):
+        super().__init__(PARAMS_SHORTINT_1BIT, seed, threads, raw)
+        self.L = self.p["n"] + 1
+        self.G = (self.p["k"] + 1) * self.p["N"]
+
+    def s1_encrypt(self, bits, seed: bytes, start_index: int = 0) -> np.ndarray:
+        out = np.zeros((len(bits), self.L), dtype=np.uint64)
+        for i, b in enumerate(bits):
+            lib().or_s1_encrypt(self.ck, seed, start_index + i, int(b), _p64(out[i]))
+        return out
+
+    def s1_decrypt(self, cts: np.ndarray) -> np.ndarray:
+        cts = np.ascontiguousarray(cts, dtype=np.uint64).reshape(-1, self.L)
+        return np.array([lib().or_s1_decrypt(self.ck, _p64(cts[i])) for i in range(cts.shape[0])], dtype=np.uint8)
+
+    def glwe_decrypt(self, glwe: np.ndarray) -> np.ndarray:
+        out = np.zeros(self.p["N"], dtype=np.uint64)
+        lib().or_glwe_decrypt(self.ck, _p64(np.ascontiguousarray(glwe, dtype=np.uint64)), _p64(out))
+        return out
+
+    def tv_from_fn(self, f0: int, f1: int) -> np.ndarray:
+        out = np.zeros(self.G, dtype=np.uint64)
+        lib().or_s1_tv_from_fn(self.p["k"], self.p["N"], f0, f1, _p64(out))
+        return out
+
+    def pks(self, ct: np.ndarray) -> np.ndarray:
+        out = np.zeros(self.G, dtype=np.uint64)
+        lib().or_s1_pks(self.sk, _p64(np.ascontiguousarray(ct, dtype=np.uint64)), _p64(out))
+        return out
+
+    def pack(self, cts: np.ndarray) -> np.ndarray:
+        cts = np.ascontiguousarray(cts, dtype=np.uint64).reshape(-1, self.L)
+        out = np.zeros(self.G, dtype=np.uint64)
+        lib().or_s1_pack(self.sk, _p64(cts), cts.shape[0], _p64(out))
+        return out
+
+    def tv_from_cts(self, ct0: np.ndarray, ct1: np.ndarray) -> np.ndarray:
+        out = np.zeros(self.G, dtype=np.uint64)
+        lib().or_s1_tv_from_cts(self.sk, _p64(np.ascontiguousarray(ct0, dtype=np.uint64)),
+                                _p64(np.ascontiguousarray(ct1, dtype=np.uint64)), _p64(out))
+        return out
+
+    def bootstrap(self, ct: np.ndarray, tv: np.ndarray) -> np.ndarray:
+        out = np.zeros(self.L, dtype=np.uint64)
+        lib().or_s1_bootstrap(self.sk, _p64(np.ascontiguousarray(ct, dtype=np.uint64)),
+                              _p64(np.ascontiguousarray(tv, dtype=np.uint64)), _p64(out))
+        return out
+
+    def multivariate(self, bits: np.ndarray, f_table) -> np.ndarray:
+        bits = np.ascontiguousarray(bits, dtype=np.uint64).reshape(-1, self.L)
+        tab = np.ascontiguousarray(np.array(f_table, dtype=np.uint64))
+        assert len(tab) == 1 << bits.shape[0]
+        out = np.zeros(self.L, dtype=np.uint64)
+        lib().or_s1_multivariate(self.sk, _p64(bits), bits.shape[0], _p64(tab), _p64(out))
         return out
 
 

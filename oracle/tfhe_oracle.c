@@ -45,6 +45,13 @@ int or_params_get(int id, or_params *o) {
                          1.5140301927925663e-05, 0.00000000000000022148688116005568,
                          0.00000000000000022148688116005568, 11};
         return 0;
+    case 5: /* shortint_1bit PARAMS, src/tfhe/shortint_1bit.rs:62-83 (ClassicPBSParameters "testing
+             * parameters"; message modulus 2, carry 1, MaxNoiseLevel 11, EncryptionKeyChoice::Small).
+             * The packing keyswitch key of generate_keys_with_params (:186-196) uses ks_base_log /
+             * ks_level and the lwe noise: stored as (pfks_l, pfks_b, pfks_std). No CBS. */
+        *o = (or_params){640, 4, 512, 7, 6, 2, 6, 0, 0, 2, 6,
+                         4.728000245054929e-7, 2.845267479601915e-15, 4.728000245054929e-7, 11, 2};
+        return 0;
     default:
         return -1;
     }
@@ -501,6 +508,7 @@ size_t or_bsk_len(const or_params *p) {
     return (size_t)p->n * p->pbs_l * (p->k + 1) * (p->k + 1) * p->N;
 }
 size_t or_pfpksk_len(const or_params *p) {
+    if (p->model == 2) return (size_t)p->n * p->pfks_l * (p->k + 1) * p->N; /* packing keyswitch key */
     return (size_t)(p->k + 1) * (p->k * p->N + 1) * p->pfks_l * (p->k + 1) * p->N;
 }
 
@@ -538,6 +546,19 @@ static void *kg_worker(void *arg) {
             msg[0] = 0 - factor;
         }
         glwe_encrypt(J->glwe_sk, k, N, msg, p->glwe_std, J->seed, P_BSK, c, J->bsk + c * glwe);
+    }
+    if (p->model == 2) {
+        /* shortint_1bit: lwe_packing_keyswitch_key_generation (shortint_1bit.rs:186-196): input key
+         * element i, level l: GLWE encryption of the constant polynomial s_i * 2^(64 - B l) */
+        for (size_t c = J->tid; c < (size_t)n * p->pfks_l; c += J->nthreads) {
+            size_t i = c / p->pfks_l;
+            int l = (int)(c % p->pfks_l) + 1;
+            memset(msg, 0, sizeof(uint64_t) * N);
+            msg[0] = J->lwe_sk[i] << (64 - p->pfks_b * l);
+            glwe_encrypt(J->glwe_sk, k, N, msg, p->pfks_std, J->seed, P_PFPKSK, c, J->pfpksk + c * glwe);
+        }
+        free(msg);
+        return NULL;
     }
     /* PFPKSK list (circuit_bootstrap_lwe_pfpksk_list): key q, input i (s_K = -1), level l:
      * plaintext = P_q * (-s_i) * 2^(64 - B l), P_q = S_q (q<k) or the constant -1 (q=k). */
@@ -1315,4 +1336,138 @@ void or_aes8_encrypt_block(const or_server_key *sk, const uint64_t *rk, const ui
     memcpy(out, state, sizeof(uint64_t) * 16 * byte_sz);
     free(state);
     free(sb);
+}
+
+/* ======================================================================================
+ * shortint_1bit model (src/tfhe/shortint_1bit.rs; AES driver src/aes_128/fhe/fhe_impls/shortint_1bit.rs)
+ * Bits are shortint ciphertexts under the SMALL key (EncryptionKeyChoice::Small), message m * 2^62
+ * (message modulus 2, carry 1: delta = 2^63 / 2).
+ * ====================================================================================== */
+/* shortint ClientKey::encrypt (shortint_1bit.rs:157-160 -> tfhe shortint encrypt, Small key, lwe noise) */
+void or_s1_encrypt(const or_client_key *ck, const uint8_t seed[32], uint64_t index, uint64_t bit, uint64_t *out) {
+    lwe_encrypt(ck->lwe_sk, ck->p.n, (bit & 1) << 62, ck->p.lwe_std, seed, P_ENCRYPT, index, out);
+}
+/* shortint decrypt_message_and_carry % message_modulus: (x + ((x & delta/2) << 1)) / delta mod 2 */
+uint64_t or_s1_decrypt(const or_client_key *ck, const uint64_t *ct) {
+    uint64_t x = or_decrypt_small_phase(ck, ct);
+    uint64_t rounding = (x & (1ull << 61)) << 1;
+    return ((x + rounding) >> 62) & 1;
+}
+
+/* test_vector_from_cleartext_fn (shortint_1bit.rs:349-373): body[0..N/2) = encode(f(0)),
+ * body[N/2..N) = encode(f(1)), encode_bit = m << 62 (:339-343), then rotate_left(N/4) */
+void or_s1_tv_from_fn(int k, int N, uint64_t f0, uint64_t f1, uint64_t *glwe) {
+    memset(glwe, 0, sizeof(uint64_t) * (size_t)(k + 1) * N);
+    uint64_t *body = glwe + (size_t)k * N;
+    uint64_t *tmp = (uint64_t *)malloc(sizeof(uint64_t) * N);
+    int box = N / 2, half = box / 2;
+    for (int j = 0; j < N; j++) tmp[j] = (j < box ? (f0 & 1) : (f1 & 1)) << 62;
+    for (int j = 0; j < N; j++) body[j] = tmp[(j + half) % N]; /* slice::rotate_left(half) */
+    free(tmp);
+}
+
+/* tfhe-rs keyswitch_lwe_ciphertext_into_glwe_ciphertext: out = 0, body[0] = b, then
+ * out -= sum_{i<n} sum_l d_{i,l} * PKSK[i][l] (decomposition of each mask element, levels 1..l) */
+void or_s1_pks(const or_server_key *sk, const uint64_t *in, uint64_t *out) {
+    const or_params *p = &sk->p;
+    int n = p->n;
+    size_t glwe = (size_t)(p->k + 1) * p->N;
+    int64_t d[64];
+    memset(out, 0, sizeof(uint64_t) * glwe);
+    out[(size_t)p->k * p->N] = in[n];
+    for (int i = 0; i < n; i++) {
+        or_decompose(in[i], p->pfks_b, p->pfks_l, d);
+        for (int l = 0; l < p->pfks_l; l++) {
+            if (!d[l]) continue;
+            const uint64_t *key = sk->pfpksk + ((size_t)i * p->pfks_l + l) * glwe;
+            uint64_t dv = (uint64_t)d[l];
+            for (size_t t = 0; t < glwe; t++) out[t] -= key[t] * dv;
+        }
+    }
+}
+
+static void glwe_monomial_mul(const or_params *p, uint64_t *g, int64_t degree) {
+    uint64_t *tmp = (uint64_t *)malloc(sizeof(uint64_t) * p->N);
+    for (int c = 0; c <= p->k; c++) {
+        or_monomial_mul(g + (size_t)c * p->N, tmp, p->N, degree);
+        memcpy(g + (size_t)c * p->N, tmp, sizeof(uint64_t) * p->N);
+    }
+    free(tmp);
+}
+static void glwe_add(const or_params *p, uint64_t *a, const uint64_t *b) {
+    for (size_t t = 0; t < (size_t)(p->k + 1) * p->N; t++) a[t] += b[t];
+}
+
+/* keyswitch_lwe_ciphertext_list_and_pack_in_glwe_ciphertext: ciphertext #j keyswitched, times X^j, summed */
+void or_s1_pack(const or_server_key *sk, const uint64_t *cts, int count, uint64_t *out) {
+    const or_params *p = &sk->p;
+    size_t glwe = (size_t)(p->k + 1) * p->N;
+    uint64_t *buf = (uint64_t *)malloc(sizeof(uint64_t) * glwe);
+    memset(out, 0, sizeof(uint64_t) * glwe);
+    for (int j = 0; j < count; j++) {
+        or_s1_pks(sk, cts + (size_t)j * (p->n + 1), buf);
+        glwe_monomial_mul(p, buf, j);
+        glwe_add(p, out, buf);
+    }
+    free(buf);
+}
+
+/* test_vector_from_ciphertexts (shortint_1bit.rs:375-466), step by step as the reference writes it:
+ * ct0 fills coefficients [0, N/4) and [3N/4, N), ct1 fills [N/4, 3N/4) */
+void or_s1_tv_from_cts(const or_server_key *sk, const uint64_t *ct0, const uint64_t *ct1, uint64_t *tv) {
+    const or_params *p = &sk->p;
+    int N = p->N, box = N / 2, half = box / 2;
+    size_t glwe = (size_t)(p->k + 1) * N;
+    uint64_t *buf = (uint64_t *)malloc(sizeof(uint64_t) * glwe);
+    memset(tv, 0, sizeof(uint64_t) * glwe);
+    or_s1_pks(sk, ct0, buf);
+    for (int i = 0; i < half; i++) {
+        glwe_add(p, tv, buf);
+        glwe_monomial_mul(p, buf, 1);
+    }
+    glwe_monomial_mul(p, buf, N - half - half);
+    for (int i = N - half; i < N; i++) {
+        glwe_add(p, tv, buf);
+        glwe_monomial_mul(p, buf, 1);
+    }
+    or_s1_pks(sk, ct1, buf);
+    glwe_monomial_mul(p, buf, half);
+    for (int i = half; i < N - half; i++) {
+        glwe_add(p, tv, buf);
+        glwe_monomial_mul(p, buf, 1);
+    }
+    free(buf);
+}
+
+/* FheContext::bootstrap_assign (shortint_1bit.rs:257-286): apply_programmable_bootstrap (blind
+ * rotation of the test vector, sample extraction) then keyswitch_lwe_ciphertext to the small key */
+void or_s1_bootstrap(const or_server_key *sk, const uint64_t *in, const uint64_t *tv, uint64_t *out) {
+    const or_params *p = &sk->p;
+    uint64_t *big = (uint64_t *)malloc(sizeof(uint64_t) * ((size_t)p->k * p->N + 1));
+    or_bootstrap(sk, in, tv, big);
+    or_keyswitch(sk, big, out);
+    free(big);
+}
+
+/* generate_multivariate_test_vector (:478-495) + calculate_multivariate_function / apply_selectors_rec
+ * (:497-536): the last bit selects inside each test vector, the results are packed pairwise into the
+ * next level's test vectors (test_vector_from_ciphertexts), the next-to-last bit selects among those... */
+void or_s1_multivariate(const or_server_key *sk, const uint64_t *bits, int nbits, const uint64_t *f_table,
+                        uint64_t *out) {
+    const or_params *p = &sk->p;
+    size_t glwe = (size_t)(p->k + 1) * p->N, L = (size_t)p->n + 1;
+    int ntv = 1 << (nbits - 1);
+    uint64_t *tvs = (uint64_t *)malloc(sizeof(uint64_t) * glwe * ntv);
+    uint64_t *res = (uint64_t *)malloc(sizeof(uint64_t) * L * ntv);
+    for (int v = 0; v < ntv; v++) or_s1_tv_from_fn(p->k, p->N, f_table[2 * v], f_table[2 * v + 1], tvs + v * glwe);
+    for (int sel = nbits - 1;; sel--) {
+        const uint64_t *selector = bits + (size_t)sel * L;
+        for (int v = 0; v < ntv; v++) or_s1_bootstrap(sk, selector, tvs + v * glwe, res + v * L);
+        if (ntv == 1) break;
+        ntv /= 2;
+        for (int v = 0; v < ntv; v++) or_s1_tv_from_cts(sk, res + 2 * v * L, res + (2 * v + 1) * L, tvs + v * glwe);
+    }
+    memcpy(out, res, sizeof(uint64_t) * L);
+    free(tvs);
+    free(res);
 }

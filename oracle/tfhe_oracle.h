@@ -52,10 +52,13 @@ typedef struct {
     int pfks_l, pfks_b;
     double lwe_std, glwe_std, pfks_std;
     uint64_t max_noise_sq;
+    int model; /* 0: WoP-PBS models (ids 0-4); 2: shortint_1bit (id 5): pfpksk holds the packing
+                * keyswitch key [n][pfks_l][(k+1)N], (pfks_l, pfks_b) = (ks_l, ks_b) */
 } or_params;
 
 /* 0 = params_sqrd_lvl_1 (:29), 1 = _4 (:77), 2 = _64 (:125), 3 = _256 (:173),
- * 4 = shortint_woppbs_8bit params() (shortint_woppbs_8bit.rs:39-86) */
+ * 4 = shortint_woppbs_8bit params() (shortint_woppbs_8bit.rs:39-86),
+ * 5 = shortint_1bit PARAMS (src/tfhe/shortint_1bit.rs:62-83) */
 int or_params_get(int id, or_params *out);
 
 /* ---------------- randomness (keygen spec shared with the product) ---------- */
@@ -162,6 +165,24 @@ void or_encrypt_int(const or_client_key *ck, const uint8_t seed[32], uint64_t in
 uint64_t or_decrypt_int(const or_client_key *ck, const uint64_t *ct);
 void or_generate_lut_without_padding(int N, const uint64_t *f_table /*[256]*/, uint64_t *out /*[max(N,256)]*/);
 void or_extract_bits(const or_server_key *sk, const uint64_t *lwe_in, int delta_log, int nbits, uint64_t *out);
+/* ---------------- shortint_1bit model (param id 5: src/tfhe/shortint_1bit.rs) ---------------- */
+/* shortint encrypt / decrypt, message modulus 2, carry 1, EncryptionKeyChoice::Small: [n+1] */
+void or_s1_encrypt(const or_client_key *ck, const uint8_t seed[32], uint64_t index, uint64_t bit, uint64_t *out);
+uint64_t or_s1_decrypt(const or_client_key *ck, const uint64_t *ct);
+/* test_vector_from_cleartext_fn (:349-373): trivial GLWE, boxes f(0) / f(1) rotated left by N/4 */
+void or_s1_tv_from_fn(int k, int N, uint64_t f0, uint64_t f1, uint64_t *glwe);
+/* keyswitch_lwe_ciphertext_into_glwe_ciphertext with the packing keyswitch key: [n+1] -> [(k+1)N] */
+void or_s1_pks(const or_server_key *sk, const uint64_t *in, uint64_t *glwe);
+/* keyswitch_lwe_ciphertext_list_and_pack_in_glwe_ciphertext (FheContext::packing_keyswitch :234-248) */
+void or_s1_pack(const or_server_key *sk, const uint64_t *cts, int count, uint64_t *glwe);
+/* test_vector_from_ciphertexts (:375-466) */
+void or_s1_tv_from_cts(const or_server_key *sk, const uint64_t *ct0, const uint64_t *ct1, uint64_t *glwe);
+/* FheContext::bootstrap (:250-286): PBS with a test vector, then keyswitch back to the small key */
+void or_s1_bootstrap(const or_server_key *sk, const uint64_t *in, const uint64_t *tv, uint64_t *out);
+/* calculate_multivariate_function (:497-536) over bits [nbits][n+1] (MSB first) with the test vectors of
+ * generate_multivariate_test_vector (:478-495) for f_table [2^nbits] (0/1 values) */
+void or_s1_multivariate(const or_server_key *sk, const uint64_t *bits, int nbits, const uint64_t *f_table,
+                        uint64_t *out);
 void or_bootstrap_with_lut8(const or_server_key *sk, const uint64_t *bits, const uint64_t *lut, uint64_t *out);
 void or_gf_256_mul_terms(uint8_t b, int coef[8][8]);
 void or_mix_column_terms(int coef[32][32]);

@@ -9,10 +9,13 @@ from tfhe_aes import Cleartext, aes_128
 
 def test_params_match_reference(oracle_mod):
     # parameters.rs:29-205
-    for pid in range(5):
+    for pid in range(6):
         prod = tfhe_aes.get_params(pid)
-        assert prod.pop("model") == (8 if pid == tfhe_aes.PARAMS_WOPPBS_8BIT else 1)
-        assert prod == oracle_mod.params(pid)
+        model = prod.pop("model")
+        assert model == {tfhe_aes.PARAMS_WOPPBS_8BIT: 8, tfhe_aes.PARAMS_SHORTINT_1BIT: 2}.get(pid, 1)
+        ref = oracle_mod.params(pid)
+        assert ref.pop("model") == (2 if model == 2 else 0)
+        assert prod == ref
     p = tfhe_aes.get_params(tfhe_aes.PARAMS_SQRD_LVL_64)
     assert (p["n"], p["k"], p["N"], p["pbs_l"], p["pbs_b"], p["ks_l"], p["ks_b"], p["cbs_l"], p["cbs_b"],
             p["pfks_l"], p["pfks_b"], p["max_noise_sq"]) == (677, 4, 512, 3, 12, 4, 3, 1, 13, 2, 16, 64)

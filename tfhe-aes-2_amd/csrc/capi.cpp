@@ -164,7 +164,7 @@ int tae_bit_len(int param_set, size_t *len) {
     return guarded([&] {
         require(len, "null");
         const tae::Params p = params_of(param_set);
-        *len = p.model == 8 ? p.small_len() : p.big_len();
+        *len = p.bit_len();
     });
 }
 
@@ -311,7 +311,9 @@ int tae_encrypt(const tae_client_key *ck, uint64_t bit, tae_bit **out) {
         b->b.ct.assign(c.bit_len(), 0);
         c.encrypt_model_bit_at(bit, tae::kAutoIndexBase + c.next_index.fetch_add(1), b->b.ct.data());
         // BitCt::fresh (1-bit model: noise^2 1 + a new component id; 8-bit: NoiseLevel::NOMINAL)
-        b->b.noise = c.p.model == 8 ? tae::NoiseLevel{1, {}} : tae::NoiseLevel::with_noise_level(1, tae::next_ct_id());
+        b->b.noise = c.p.model == 8   ? tae::NoiseLevel{1, {}}
+                     : c.p.model == 2 ? tae::NoiseLevel{}  // shortint_1bit: unchecked adds, nothing tracked
+                                      : tae::NoiseLevel::with_noise_level(1, tae::next_ct_id());
         b->b.max_noise_sq = c.p.max_noise_sq;
         *out = b.release();
     });
@@ -614,6 +616,7 @@ int tae_aes_noise_schedule_check(int param_set, int driver, int rounds) {
         const tae::Params p = params_of(param_set);
         require(driver == TAE_DRIVER_GAL_MUL || driver == TAE_DRIVER_SBOX_PBS, "unknown driver");
         if (rounds < 1 || rounds > 10) throw tae::ModelError{TAE_E_PARAM, "rounds must be in 1..=10"};
+        if (p.model == 2) return;  // shortint_1bit: unchecked adds, no bookkeeping to fail
         std::vector<tae::NoiseLevel> rk(44 * 32), blk(128);
         for (auto &x : rk) x = p.model == 8 ? tae::NoiseLevel{1, {}} : tae::NoiseLevel::with_noise_level(1, tae::next_ct_id());
         for (auto &x : blk) x = p.model == 8 ? tae::NoiseLevel{1, {}} : tae::NoiseLevel::with_noise_level(1, tae::next_ct_id());
@@ -626,6 +629,48 @@ int tae_aes_noise_schedule_check(int param_set, int driver, int rounds) {
     });
 }
 
+
+/* ---- shortint_1bit model ---- */
+int tae_s1_test_vector_from_fn(int param_set, uint64_t f0, uint64_t f1, uint64_t *tv) {
+    return guarded([&] {
+        require(tv, "null");
+        const tae::Params p = params_of(param_set);
+        require(p.model == 2, "test vectors belong to the shortint_1bit parameter set");
+        require(f0 <= 1 && f1 <= 1, "function values must be 0 or 1");
+        tae::s1_test_vector(p, f0, f1, tv);
+    });
+}
+
+int tae_s1_bootstrap(const tae_context *ctx, const uint64_t *in, size_t count, const uint64_t *tvs, size_t n_tv,
+                     uint64_t *out, int mem) {
+    return guarded([&] {
+        require(ctx && (in || !count) && tvs && (out || !count), "null");
+        if (count) ctx->ctx->s1_bootstrap_raw(in, count, tvs, n_tv, out, mem == TAE_MEM_DEVICE);
+    });
+}
+
+int tae_s1_packing_keyswitch(const tae_context *ctx, const uint64_t *cts, size_t count, uint64_t *glwe, int mem) {
+    return guarded([&] {
+        require(ctx && cts && glwe, "null");
+        ctx->ctx->s1_packing_keyswitch_raw(cts, count, glwe, mem == TAE_MEM_DEVICE);
+    });
+}
+
+int tae_s1_test_vectors_from_ciphertexts(const tae_context *ctx, const uint64_t *ct0, const uint64_t *ct1, size_t count,
+                                         uint64_t *tvs, int mem) {
+    return guarded([&] {
+        require(ctx && (count == 0 || (ct0 && ct1 && tvs)), "null");
+        if (count) ctx->ctx->s1_test_vectors_from_ciphertexts_raw(ct0, ct1, count, tvs, mem == TAE_MEM_DEVICE);
+    });
+}
+
+int tae_s1_multivariate(const tae_context *ctx, const uint64_t *bits, size_t groups, int nbits,
+                        const uint64_t *f_tables, int n_fn, uint64_t *out, int mem) {
+    return guarded([&] {
+        require(ctx && f_tables && (groups == 0 || (bits && out)), "null");
+        if (groups) ctx->ctx->s1_multivariate_raw(bits, groups, nbits, f_tables, n_fn, out, mem == TAE_MEM_DEVICE);
+    });
+}
 
 int tae_stage_keyswitch(const tae_context *ctx, const uint64_t *in, size_t count, uint64_t *out, int mem) {
     return guarded([&] {

@@ -133,6 +133,10 @@ void ClientKey::encrypt_small_bit_at(uint64_t bit, uint64_t index, uint64_t *out
     lwe_encrypt(seed.data(), ENCRYPT, index, lwe_sk.data(), p.n, encode_bit(bit), p.lwe_std, out);
 }
 
+void ClientKey::encrypt_s1_bit_at(uint64_t bit, uint64_t index, uint64_t *out) const {
+    lwe_encrypt(seed.data(), ENCRYPT, index, lwe_sk.data(), p.n, (bit & 1) << 62, p.lwe_std, out);
+}
+
 uint64_t ClientKey::phase_small(const uint64_t *ct) const {
     uint64_t s = 0;
     for (int i = 0; i < p.n; i++) s += ct[i] * lwe_sk[i];
@@ -141,6 +145,16 @@ uint64_t ClientKey::phase_small(const uint64_t *ct) const {
 
 void ClientKey::encrypt_int_at(uint64_t value, uint64_t index, uint64_t *out) const {
     lwe_encrypt(seed.data(), ENCRYPT_INT, index, glwe_sk.data(), p.K(), (value & 255) << 56, p.glwe_std, out);
+}
+
+void s1_test_vector(const Params &p, uint64_t f0, uint64_t f1, uint64_t *glwe) {
+    const int N = p.N, box = N / 2, half = box / 2;
+    std::memset(glwe, 0, sizeof(uint64_t) * p.glwe_len());
+    uint64_t *body = glwe + (size_t)p.k * N;
+    for (int j = 0; j < N; j++) {
+        const int src = (j + half) % N;  // slice::rotate_left(half)
+        body[j] = (src < box ? (f0 & 1) : (f1 & 1)) << 62;
+    }
 }
 
 void generate_lut_without_padding(int N, const uint64_t *f_table, uint64_t *out) {
@@ -210,6 +224,18 @@ void generate_keys(const Params &p, const uint8_t seed[32], int threads, ClientK
             msg[0] = 0 - factor;
         glwe_encrypt(seed, BSK, c, S, k, N, msg.data(), p.glwe_std, sk.bsk.data() + c * glwe);
     });
+    if (p.model == 2) {
+        // shortint_1bit: lwe_packing_keyswitch_key_generation (shortint_1bit.rs:186-196): input key
+        // element i, level l: GLWE encryption of the constant polynomial s_i * 2^(64 - pfks_b*l)
+        parallel_for((size_t)n * p.pfks_l, threads, [&](size_t c) {
+            std::vector<uint64_t> msg(N, 0);
+            const size_t i = c / p.pfks_l;
+            const int l = (int)(c % p.pfks_l) + 1;
+            msg[0] = ck.lwe_sk[i] << (64 - p.pfks_b * l);
+            glwe_encrypt(seed, PFPKSK, c, S, k, N, msg.data(), p.pfks_std, sk.pfpksk.data() + c * glwe);
+        });
+        return;
+    }
     // PFPKSK list (circuit_bootstrap_lwe_pfpksk_list, f(x) = -x): key q, input i (s_K = -1),
     // level l: plaintext P_q * (-s_i) * 2^(64 - pfks_b*l), P_q = S_q (q<k) or the constant -1.
     parallel_for((size_t)(k + 1) * (K + 1) * p.pfks_l, threads, [&](size_t c) {

@@ -80,16 +80,23 @@ struct ClientKey {
     // big-key LWE of m * 2^56 with glwe noise (the FullWidthCiphertext of the 8-bit model)
     void encrypt_int_at(uint64_t value, uint64_t index, uint64_t *out) const;
     uint64_t decrypt_int(const uint64_t *ct) const { return ((phase(ct) + (1ull << 55)) >> 56) & 255; }
-    // bits of either model: big key (model 1) or small key (model 8)
-    size_t bit_len() const { return p.model == 8 ? p.small_len() : p.big_len(); }
+    // shortint_1bit model (shortint_1bit.rs:149-161): shortint encrypt / decrypt with message modulus 2,
+    // carry 1 under the SMALL key: plaintext m * 2^62, decrypt_message_and_carry % 2
+    void encrypt_s1_bit_at(uint64_t bit, uint64_t index, uint64_t *out) const;
+    uint64_t decrypt_s1_bit(const uint64_t *ct) const { return decode_s1(phase_small(ct)); }
+    static uint64_t decode_s1(uint64_t x) { return ((x + ((x & (1ull << 61)) << 1)) >> 62) & 1; }
+    // bits of any model: big key (model 1) or small key (models 8 and 2)
+    size_t bit_len() const { return p.bit_len(); }
     void encrypt_model_bit_at(uint64_t bit, uint64_t index, uint64_t *out) const {
         if (p.model == 8)
             encrypt_small_bit_at(bit, index, out);
+        else if (p.model == 2)
+            encrypt_s1_bit_at(bit, index, out);
         else
             encrypt_bit_at(bit, index, out);
     }
     uint64_t decrypt_model_bit(const uint64_t *ct) const {
-        return p.model == 8 ? decrypt_small_bit(ct) : decrypt_bit(ct);
+        return p.model == 8 ? decrypt_small_bit(ct) : p.model == 2 ? decrypt_s1_bit(ct) : decrypt_bit(ct);
     }
 };
 
@@ -107,6 +114,10 @@ void generate_lut(int N, int input_bits, int output_bits, const uint64_t *f_tabl
 // WopbsKey::generate_lut_without_padding for message modulus 256 (8-bit model,
 // shortint_woppbs_8bit.rs:262-265): out[i] = (f(i mod 256) mod 256) << 56, i < max(N, 256)
 void generate_lut_without_padding(int N, const uint64_t *f_table /*[256]*/, uint64_t *out);
+
+// shortint_1bit test_vector_from_cleartext_fn (shortint_1bit.rs:349-373) for f(0) = f0, f(1) = f1:
+// trivial GLWE [(k+1)N], body boxes encode(f0) | encode(f1) (encode_bit = m << 62) rotated left by N/4
+void s1_test_vector(const Params &p, uint64_t f0, uint64_t f1, uint64_t *glwe);
 
 // Negacyclic FFT tables (twist, untwist, W_M) -- the spec shared with the kernels.
 struct FftTables {

@@ -58,9 +58,10 @@ class Engine {
     void keyswitch(const uint64_t *d_in, uint64_t *d_out, size_t B);
     // homomorphic_shift_boolean at cbs level `level`: [B][n+1] -> [B][K+1]
     void pbs_shift_boolean(const uint64_t *d_small, uint64_t *d_big, size_t B, int level);
-    // generic FourierLweBootstrapKey::bootstrap with a per-batch LUT GLWE [(k+1)N]
+    // generic FourierLweBootstrapKey::bootstrap with LUT GLWEs [(k+1)N]: ciphertext b takes
+    // d_lut_glwe + (b % lut_mod) (k+1)N (lut_mod 1: one LUT for the batch; > 1 only on the generic kernel)
     void bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint64_t *d_big, size_t B,
-                   uint64_t body_add, uint64_t out_add);
+                   uint64_t body_add, uint64_t out_add, size_t lut_mod = 1);
     // private functional keyswitches of level `level`: [B][K+1] -> GGSW rows of that level in
     // d_ggsw [B][cbs_l][k+1][(k+1)N]
     void pfks_into_ggsw(const uint64_t *d_big, uint64_t *d_ggsw, size_t B, int level);
@@ -95,6 +96,25 @@ class Engine {
     // rk [44*32][K+1] (expanded key words, word-major, MSB-first bits), blocks [nb][128][K+1]
     void aes_encrypt_blocks(const uint64_t *d_rk, const uint64_t *d_blocks, size_t nb, int rounds,
                             uint64_t *d_out);
+
+    // ---- shortint_1bit model (src/tfhe/shortint_1bit.rs; param set SHORTINT_1BIT) ----
+    // FheContext::bootstrap (:250-286): PBS with test vector d_tvs + (b % lut_mod) (k+1)N, then the keyswitch
+    // back to the small key: [B][n+1] -> [B][n+1]
+    void s1_bootstrap(const uint64_t *d_in, const uint64_t *d_tvs, size_t lut_mod, uint64_t *d_out, size_t B);
+    // keyswitch_lwe_ciphertext_into_glwe_ciphertext with the packing key, per ciphertext: [B][n+1] -> [B][(k+1)N]
+    void s1_pks(const uint64_t *d_in, size_t B, uint64_t *d_out);
+    // test_vector_from_ciphertexts (:375-466) over P pairs of packing keyswitches [2P][(k+1)N] -> [P][(k+1)N]
+    void s1_tv_from_pks(const uint64_t *d_pks, size_t P, uint64_t *d_tv);
+    // FheContext::packing_keyswitch (:234-248): count ciphertexts into one GLWE, #j at X^j
+    void s1_pack(const uint64_t *d_in, int count, uint64_t *d_out);
+    // calculate_multivariate_function (:497-536) for n_fn functions of the same nbits bits, over G groups:
+    // bits [G][nbits][n+1] (MSB first), d_tvs [n_fn][2^(nbits-1)][(k+1)N] (generate_multivariate_test_vector)
+    // -> [G][n_fn][n+1]; one batched bootstrap + packing step per selector level
+    void s1_multivariate(const uint64_t *d_bits, size_t G, int nbits, const uint64_t *d_tvs, int n_fn, uint64_t *d_out);
+    // Shortint1BitSboxPbsAesEncrypt::encrypt_block_for_rounds over nb blocks: rk [44*32][n+1], blocks [nb][128][n+1]
+    void s1_aes_encrypt_blocks(const uint64_t *d_rk, const uint64_t *d_blocks, size_t nb, int rounds, uint64_t *d_out);
+    const uint64_t *s1_sbox_tvs() const { return d_s1_sbox_tv_; }  // [8][128][(k+1)N]
+    const uint64_t *s1_identity_tv() const { return d_s1_id_tv_; }  // [(k+1)N]
 
     // ---- element-wise helpers ----
     void lwe_add(uint64_t *d_a, const uint64_t *d_b, size_t count);  // a += b (count u64)
@@ -138,6 +158,11 @@ class Engine {
     uint64_t *d_xbuf_ = nullptr, *d_xsh_ = nullptr, *d_xks_ = nullptr, *d_xpbs_ = nullptr, *d_ints_ = nullptr;
     size_t cap_xbuf_ = 0, cap_xsh_ = 0, cap_xks_ = 0, cap_xpbs_ = 0, cap_ints_ = 0;
     int8_t mix_idx_[32][8] = {};
+    // shortint_1bit: S-box / identity test vectors and tree-level scratch
+    uint64_t *d_s1_sbox_tv_ = nullptr, *d_s1_id_tv_ = nullptr, *d_s1_in_ = nullptr, *d_s1_out_ = nullptr,
+             *d_s1_pks_ = nullptr, *d_s1_tv_ = nullptr;
+    size_t cap_s1_in_ = 0, cap_s1_out_ = 0, cap_s1_pks_ = 0, cap_s1_tv_ = 0;
+    void require_s1() const;
     void cbs_vp_stages(const uint64_t *d_small_bits, size_t G, int n_in, const uint64_t *d_lut, int n_out,
                        uint64_t *d_out);
     // scratch

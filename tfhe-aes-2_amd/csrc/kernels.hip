@@ -175,7 +175,7 @@ __global__ void __launch_bounds__(kThreads) pbs_kernel(const uint64_t *__restric
                                                     const uint64_t *__restrict__ lut, const cplx *__restrict__ bsk,
                                                     const cplx *__restrict__ twist, const cplx *__restrict__ untwist,
                                                     const cplx *__restrict__ w, int n, int k, int levels, int base_log,
-                                                    uint64_t body_add, uint64_t out_add) {
+                                                    uint64_t body_add, uint64_t out_add, size_t lut_mod, size_t ct_off) {
     constexpr int M = N / 2;
     constexpr int logN = (N == 512) ? 9 : 10;
     extern __shared__ __align__(16) unsigned char smem[];
@@ -183,6 +183,7 @@ __global__ void __launch_bounds__(kThreads) pbs_kernel(const uint64_t *__restric
     cplx *X = reinterpret_cast<cplx *>(acc + (k + 1) * N);
     cplx *Y = X + (k + 1) * M;
     const uint64_t *in = lwe_in + (size_t)blockIdx.x * (n + 1);
+    lut += ((ct_off + blockIdx.x) % lut_mod) * (size_t)(k + 1) * N;  // this ciphertext's test vector
     const int bt = mod_switch(in[n] + body_add, logN);
     const int e0 = (2 * N - (bt % (2 * N))) % (2 * N);  // X^{-b~}
     for (int t = threadIdx.x; t < (k + 1) * N; t += blockDim.x) {
@@ -533,6 +534,62 @@ __global__ void aes8_mix_kernel(const uint64_t *__restrict__ sb, const uint64_t 
     }
 }
 
+// ---- shortint_1bit model (src/tfhe/shortint_1bit.rs) ----
+// test_vector_from_ciphertexts (:375-466) for pair p: with P0 / P1 the packing keyswitches of the two
+// ciphertexts, tv = sum_{i in [0, N/4) u [3N/4, N)} X^i P0 + sum_{i in [N/4, 3N/4)} X^i P1 (negacyclic,
+// wrapping u64: the reference's add-then-rotate loops in closed form).  One workgroup per (pair, polynomial).
+template <int N>
+__global__ void __launch_bounds__(kThreads) s1_tv_kernel(const uint64_t *__restrict__ pks, uint64_t *__restrict__ tv, int k) {
+    __shared__ uint64_t a[N], b[N];
+    const size_t pair = blockIdx.x / (k + 1);
+    const int c = blockIdx.x - (int)pair * (k + 1);
+    const size_t glwe = (size_t)(k + 1) * N;
+    const uint64_t *p0 = pks + 2 * pair * glwe + (size_t)c * N, *p1 = p0 + glwe;
+    for (int t = threadIdx.x; t < N; t += blockDim.x) {
+        a[t] = p0[t];
+        b[t] = p1[t];
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < N; t += blockDim.x) {
+        uint64_t acc = 0;
+        for (int i = 0; i < N; i++) {
+            const int src = t - i;
+            const bool wrap = src < 0;
+            const uint64_t v = (i < N / 4 || i >= 3 * N / 4) ? a[wrap ? src + N : src] : b[wrap ? src + N : src];
+            acc += wrap ? (0 - v) : v;
+        }
+        tv[pair * glwe + (size_t)c * N + t] = acc;
+    }
+}
+
+// keyswitch_lwe_ciphertext_list_and_pack_in_glwe_ciphertext: out = sum_j X^j P_j over count keyswitched
+// GLWEs P_j (one workgroup per polynomial)
+template <int N>
+__global__ void __launch_bounds__(kThreads) s1_pack_kernel(const uint64_t *__restrict__ pks, int count, uint64_t *__restrict__ out,
+                                                        int k) {
+    const int c = blockIdx.x;
+    const size_t glwe = (size_t)(k + 1) * N;
+    for (int t = threadIdx.x; t < N; t += blockDim.x) {
+        uint64_t acc = 0;
+        for (int j = 0; j < count; j++) {
+            const int src = t - j;
+            const uint64_t v = pks[(size_t)j * glwe + (size_t)c * N + (src < 0 ? src + N : src)];
+            acc += src < 0 ? (0 - v) : v;
+        }
+        out[(size_t)c * N + t] = acc;
+    }
+}
+
+// row b of out = row (b / reps) * stride + sel of in (the selector bit of each bootstrap of a tree level)
+__global__ void s1_gather_kernel(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, size_t rows, size_t reps,
+                                 int stride, int sel, int L) {
+    const size_t total = rows * (size_t)L;
+    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = t / L, j = t - r * L;
+        out[t] = in[((r / reps) * stride + sel) * (size_t)L + j];
+    }
+}
+
 unsigned grid_for(size_t total) { return (unsigned)std::min<size_t>((total + kThreads - 1) / kThreads, 65536); }
 
 constexpr int kBrC = 3;  // ciphertexts per workgroup in the batched N=512 blind rotation
@@ -578,7 +635,7 @@ void Engine::init_common() {
     HIPC(hipMemcpy(d_untwist_, t.untwist.data(), tb, hipMemcpyHostToDevice));
     HIPC(hipMemcpy(d_w_, t.w.data(), tb, hipMemcpyHostToDevice));
     // homomorphic_shift_boolean accumulators: body = -alpha, alpha = 2^(63 - cbs_b * level)
-    std::vector<uint64_t> luts((size_t)p_.cbs_l * p_.glwe_len(), 0);
+    std::vector<uint64_t> luts((size_t)std::max(p_.cbs_l, 1) * p_.glwe_len(), 0);
     for (int lev = 1; lev <= p_.cbs_l; lev++) {
         const uint64_t alpha = 1ull << (63 - p_.cbs_b * lev);
         for (int j = 0; j < p_.N; j++) luts[(size_t)(lev - 1) * p_.glwe_len() + (size_t)p_.k * p_.N + j] = 0 - alpha;
@@ -599,6 +656,36 @@ void Engine::init_common() {
     d_lut8_ = static_cast<uint64_t *>(alloc(l8.size() * 8));
     HIPC(hipMemcpy(d_lut24_, l24.data(), l24.size() * 8, hipMemcpyHostToDevice));
     HIPC(hipMemcpy(d_lut8_, l8.data(), l8.size() * 8, hipMemcpyHostToDevice));
+    if (p_.model == 2) {
+        // shortint_1bit ByteT (fhe_impls/shortint_1bit.rs:17-50): bootstrap_assign's identity test vector
+        // and sbox_substitute's 8 multivariate test vectors (one per output bit, MSB first), each the
+        // 128 cleartext test vectors of generate_multivariate_test_vector (shortint_1bit.rs:478-495)
+        const size_t glwe = p_.glwe_len(), V = 128;
+        std::vector<uint64_t> tvs(8 * V * glwe), id(glwe);
+        for (int f = 0; f < 8; f++)
+            for (size_t v = 0; v < V; v++) {
+                const uint8_t s0 = kSbox[2 * v], s1 = kSbox[2 * v + 1];
+                s1_test_vector(p_, (s0 >> (7 - f)) & 1, (s1 >> (7 - f)) & 1, &tvs[(f * V + v) * glwe]);
+            }
+        s1_test_vector(p_, 0, 1, id.data());
+        d_s1_sbox_tv_ = static_cast<uint64_t *>(alloc(tvs.size() * 8));
+        d_s1_id_tv_ = static_cast<uint64_t *>(alloc(id.size() * 8));
+        HIPC(hipMemcpy(d_s1_sbox_tv_, tvs.data(), tvs.size() * 8, hipMemcpyHostToDevice));
+        HIPC(hipMemcpy(d_s1_id_tv_, id.data(), id.size() * 8, hipMemcpyHostToDevice));
+    }
+    if (p_.model == 8 || p_.model == 2) {
+        int terms[32][32];
+        mix_column_terms(terms);
+        for (int o = 0; o < 32; o++) {
+            int q = 0;
+            for (int i = 0; i < 32; i++)
+                for (int c = 0; c < terms[o][i]; c++) {
+                    if (q >= 8) throw std::runtime_error("MixColumns network: more than 8 terms per bit");
+                    mix_idx_[o][q++] = (int8_t)i;
+                }
+            for (; q < 8; q++) mix_idx_[o][q] = -1;
+        }
+    }
     if (p_.model == 8) {
         // 8-bit model: SBOX / identity LUTs without padding (fhe_impls/shortint_woppbs_8bit.rs:17-35)
         std::vector<uint64_t> fs(256), fi(256), ws(std::max(p_.N, 256)), wi(std::max(p_.N, 256));
@@ -612,17 +699,6 @@ void Engine::init_common() {
         d_wlut_id_ = static_cast<uint64_t *>(alloc(wi.size() * 8));
         HIPC(hipMemcpy(d_wlut_sbox_, ws.data(), ws.size() * 8, hipMemcpyHostToDevice));
         HIPC(hipMemcpy(d_wlut_id_, wi.data(), wi.size() * 8, hipMemcpyHostToDevice));
-        int terms[32][32];
-        mix_column_terms(terms);
-        for (int o = 0; o < 32; o++) {
-            int q = 0;
-            for (int i = 0; i < 32; i++)
-                for (int c = 0; c < terms[o][i]; c++) {
-                    if (q >= 8) throw std::runtime_error("MixColumns network: more than 8 terms per bit");
-                    mix_idx_[o][q++] = (int8_t)i;
-                }
-            for (; q < 8; q++) mix_idx_[o][q] = -1;
-        }
     }
     // batched N=512, k=4 blind rotation (params_sqrd_lvl_64): br512x4 for large batches, br512lat for
     // small ones.  TAE_BR_LAT_MAX (a tuning knob, both sides pinned by tests) is the batch size up
@@ -722,6 +798,22 @@ void Engine::prepare_mfma_keys() {
     mfma_ks_ = p_.pfks_b <= 16 && p_.ks_b <= 7;
     if (!mfma_ks_) return;
     const int glwe = (int)p_.glwe_len();
+    if (p_.model == 2) {
+        // packing keyswitch (keyswitch_lwe_ciphertext_into_glwe_ciphertext) = the KS GEMM with the packing
+        // key: kd = (i, l) over n x pfks_l, col over the GLWE, the LWE body added at column kN
+        const int kd = p_.n * p_.pfks_l, nc = (p_.k + 1) * p_.N, kd_ks = p_.K() * p_.ks_l, nc_ks = p_.n + 1;
+        if (p_.pfks_b > 7) throw std::runtime_error("packing keyswitch digits must fit one byte");
+        kp_pf_ = (kd + ksgemm::TK - 1) / ksgemm::TK * ksgemm::TK;
+        kp_ks_ = (kd_ks + ksgemm::TK - 1) / ksgemm::TK * ksgemm::TK;
+        d_pf_bt_ = static_cast<int8_t *>(alloc((size_t)nc * 8 * kp_pf_));
+        d_ks_bt_ = static_cast<int8_t *>(alloc((size_t)nc_ks * 8 * kp_ks_));
+        dim3 gp((kp_pf_ + 63) / 64, (nc + 63) / 64), gks((kp_ks_ + 63) / 64, (nc_ks + 63) / 64);
+        ksgemm::prep_key<<<gp, kThreads, 0, stream_>>>(d_pfpksk_, d_pf_bt_, kd, kp_pf_, nc, nc, nc, 0);
+        ksgemm::prep_key<<<gks, kThreads, 0, stream_>>>(d_ksk_, d_ks_bt_, kd_ks, kp_ks_, nc_ks, nc_ks, nc_ks, 0);
+        HIPC(hipGetLastError());
+        HIPC(hipStreamSynchronize(stream_));
+        return;
+    }
     const int kd_pf = (p_.K() + 1) * p_.pfks_l, kd_ks = p_.K() * p_.ks_l;
     kp_pf_ = (kd_pf + ksgemm::TK - 1) / ksgemm::TK * ksgemm::TK;
     kp_ks_ = (kd_ks + ksgemm::TK - 1) / ksgemm::TK * ksgemm::TK;
@@ -790,7 +882,8 @@ Engine::~Engine() {
                     (void *)d_lut24_, (void *)d_lut8_, (void *)d_small_, (void *)d_big_, (void *)d_ggsw_,
                     (void *)d_ggsw_f_, (void *)d_state_, (void *)d_muls_, (void *)d_pf_bt_, (void *)d_ks_bt_, (void *)d_pf_corr_, (void *)d_pf_bt_kl_,
                     (void *)d_digits_, (void *)d_wlut_sbox_, (void *)d_wlut_id_, (void *)d_lut_x_, (void *)d_xbuf_,
-                    (void *)d_xsh_, (void *)d_xks_, (void *)d_xpbs_, (void *)d_ints_})
+                    (void *)d_xsh_, (void *)d_xks_, (void *)d_xpbs_, (void *)d_ints_, (void *)d_s1_sbox_tv_,
+                    (void *)d_s1_id_tv_, (void *)d_s1_in_, (void *)d_s1_out_, (void *)d_s1_pks_, (void *)d_s1_tv_})
         if (q) hipFree(q);
     for (auto &e : ev_pool_) hipEventDestroy(e);
     hipStreamDestroy(stream_);
@@ -832,8 +925,11 @@ void Engine::keyswitch(const uint64_t *d_in, uint64_t *d_out, size_t B) {
 }
 
 void Engine::bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint64_t *d_big, size_t B,
-                       uint64_t body_add, uint64_t out_add) {
+                       uint64_t body_add, uint64_t out_add, size_t lut_mod) {
     if (!B) return;
+    if (lut_mod == 0) throw std::runtime_error("bootstrap: lut_mod must be >= 1");
+    if (lut_mod > 1 && (x4_512_ || br1024_pbs_ || br1024lat_))
+        throw std::runtime_error("per-ciphertext test vectors run on the generic blind rotation only");
     if (x4_512_) {
         if ((long)B <= lat_max_) {
             br512lat::br_kernel<3, 12><<<(unsigned)B, br512lat::THREADS, br512lat::lds_bytes(3), stream_>>>(
@@ -882,11 +978,11 @@ void Engine::bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint
         if (p_.N == 512) {
             pbs_kernel<512><<<g, kThreads, br_lds_bytes<512>(p_.k, p_.pbs_l), stream_>>>(
                 d_small + off * p_.small_len(), d_big + off * p_.big_len(), d_lut_glwe, d_bsk_f_, d_twist_, d_untwist_,
-                d_w_, p_.n, p_.k, p_.pbs_l, p_.pbs_b, body_add, out_add);
+                d_w_, p_.n, p_.k, p_.pbs_l, p_.pbs_b, body_add, out_add, lut_mod, off);
         } else {
             pbs_kernel<1024><<<g, kThreads, br_lds_bytes<1024>(p_.k, p_.pbs_l), stream_>>>(
                 d_small + off * p_.small_len(), d_big + off * p_.big_len(), d_lut_glwe, d_bsk_f_, d_twist_, d_untwist_,
-                d_w_, p_.n, p_.k, p_.pbs_l, p_.pbs_b, body_add, out_add);
+                d_w_, p_.n, p_.k, p_.pbs_l, p_.pbs_b, body_add, out_add, lut_mod, off);
         }
         HIPC(hipGetLastError());
     }
@@ -1200,6 +1296,114 @@ void Engine::aes_encrypt_blocks(const uint64_t *d_rk, const uint64_t *d_blocks, 
     aes_final_kernel<<<grid_for(state_len), kThreads, 0, stream_>>>(d_muls_, d_rk + (size_t)160 * byte_stride, d_out,
                                                                      nb, L);
     HIPC(hipGetLastError());
+}
+
+// ---- shortint_1bit model ----
+void Engine::require_s1() const {
+    if (p_.model != 2) throw std::runtime_error("this stage belongs to the shortint_1bit parameter set");
+}
+
+void Engine::s1_bootstrap(const uint64_t *d_in, const uint64_t *d_tvs, size_t lut_mod, uint64_t *d_out, size_t B) {
+    require_s1();
+    if (!B) return;
+    grow(d_big_, cap_big_, B * p_.big_len());
+    timed(ST_PBS, [&] { bootstrap(d_in, d_tvs, d_big_, B, 0, 0, lut_mod); });
+    timed(ST_KS, [&] { keyswitch(d_big_, d_out, B); });
+}
+
+void Engine::s1_pks(const uint64_t *d_in, size_t B, uint64_t *d_out) {
+    require_s1();
+    if (!B) return;
+    const int L = p_.n + 1, kd = p_.n * p_.pfks_l, nc = (p_.k + 1) * p_.N;
+    ensure_digits(d_digits_, cap_digits_, B, kd, kp_pf_, stream_);
+    const size_t thr = B * (size_t)p_.n;
+    ksgemm::prep_digits<1, 8><<<(unsigned)((thr + 255) / 256), 256, 0, stream_>>>(d_in, L, d_digits_, (long)B, p_.n,
+                                                                                  kp_pf_, p_.pfks_b, p_.pfks_l);
+    const long mtiles = (long)((B + ksgemm::TM - 1) / ksgemm::TM);
+    const long ntiles = ((long)nc * 8 + ksgemm::TN - 1) / ksgemm::TN;
+    ksgemm::gemm<1, 8><<<(unsigned)(mtiles * ntiles), 256, 0, stream_>>>(d_digits_, d_pf_bt_, kp_pf_, (long)B, mtiles, nc,
+                                                                          d_out, nc, (long)B, d_in + p_.n, L, p_.k * p_.N);
+    HIPC(hipGetLastError());
+}
+
+void Engine::s1_tv_from_pks(const uint64_t *d_pks, size_t P, uint64_t *d_tv) {
+    require_s1();
+    if (!P) return;
+    s1_tv_kernel<512><<<(unsigned)(P * (p_.k + 1)), kThreads, 0, stream_>>>(d_pks, d_tv, p_.k);
+    HIPC(hipGetLastError());
+}
+
+void Engine::s1_pack(const uint64_t *d_in, int count, uint64_t *d_out) {
+    require_s1();
+    if (count < 1 || count > p_.N) throw std::runtime_error("packing keyswitch: 1..N ciphertexts");
+    grow(d_s1_pks_, cap_s1_pks_, (size_t)count * p_.glwe_len());
+    s1_pks(d_in, (size_t)count, d_s1_pks_);
+    s1_pack_kernel<512><<<(unsigned)(p_.k + 1), kThreads, 0, stream_>>>(d_s1_pks_, count, d_out, p_.k);
+    HIPC(hipGetLastError());
+}
+
+void Engine::s1_multivariate(const uint64_t *d_bits, size_t G, int nbits, const uint64_t *d_tvs, int n_fn,
+                             uint64_t *d_out) {
+    require_s1();
+    if (!G) return;
+    if (nbits < 1 || nbits > 8) throw std::runtime_error("multivariate functions take 1..8 bits");
+    const int L = p_.n + 1;
+    const size_t glwe = p_.glwe_len();
+    size_t V = (size_t)1 << (nbits - 1), B = G * n_fn * V;
+    grow(d_s1_in_, cap_s1_in_, B * L);
+    grow(d_s1_out_, cap_s1_out_, B * L);
+    grow(d_s1_pks_, cap_s1_pks_, B * glwe);
+    grow(d_s1_tv_, cap_s1_tv_, std::max<size_t>(B / 2, 1) * glwe);
+    const uint64_t *tvs = d_tvs;
+    size_t lut_mod = (size_t)n_fn * V;  // level 0: the cleartext test vectors, shared by every group
+    for (int sel = nbits - 1;; sel--) {
+        // apply_selectors_rec (shortint_1bit.rs:510-536): bootstrap every test vector of (group, fn) with
+        // the group's selector bit sel, then pack the results pairwise into the next level's vectors
+        s1_gather_kernel<<<grid_for(B * L), kThreads, 0, stream_>>>(d_bits, d_s1_in_, B, (size_t)n_fn * V, nbits, sel, L);
+        HIPC(hipGetLastError());
+        s1_bootstrap(d_s1_in_, tvs, lut_mod, V == 1 ? d_out : d_s1_out_, B);
+        if (V == 1) break;
+        timed(ST_PFKS, [&] {
+            s1_pks(d_s1_out_, B, d_s1_pks_);
+            s1_tv_from_pks(d_s1_pks_, B / 2, d_s1_tv_);
+        });
+        V /= 2;
+        B /= 2;
+        tvs = d_s1_tv_;
+        lut_mod = B;
+    }
+}
+
+// fhe_sbox_pbs::encrypt_block_for_rounds (fhe_sbox_pbs.rs:75-121) over nb blocks of shortint_1bit bits with
+// ByteT::sbox_substitute = 8 multivariate functions per byte (fhe_impls/shortint_1bit.rs:32-50); MixColumns
+// and AddRoundKey are the same LWE-addition network as the 8-bit model's (shortint unchecked_add,
+// shortint_1bit.rs:109-120)
+void Engine::s1_aes_encrypt_blocks(const uint64_t *d_rk, const uint64_t *d_blocks, size_t nb, int rounds,
+                                   uint64_t *d_out) {
+    require_s1();
+    if (!nb) return;
+    if (rounds < 1 || rounds > 10) throw std::runtime_error("rounds must be in 1..=10");
+    const int L = (int)p_.small_len();
+    const size_t state_len = nb * 128 * (size_t)L;
+    times_ = StageTimes{};
+    grow(d_state_, cap_state_, state_len);
+    grow(d_muls_, cap_muls_, state_len);
+    const size_t byte_stride = 8 * (size_t)L;
+    MixTerms T;
+    std::memcpy(T.idx, mix_idx_, sizeof(T.idx));
+    aes_ark0_kernel<<<grid_for(state_len), kThreads, 0, stream_>>>(d_blocks, d_rk, d_state_, nb, L);
+    HIPC(hipGetLastError());
+    for (int r = 1; r < rounds; r++) {
+        s1_multivariate(d_state_, nb * 16, 8, d_s1_sbox_tv_, 8, d_muls_);
+        aes8_mix_kernel<<<grid_for(state_len), kThreads, 0, stream_>>>(d_muls_, d_rk + (size_t)16 * r * byte_stride,
+                                                                        d_state_, nb, L, T);
+        HIPC(hipGetLastError());
+    }
+    s1_multivariate(d_state_, nb * 16, 8, d_s1_sbox_tv_, 8, d_muls_);
+    aes_final_kernel<<<grid_for(state_len), kThreads, 0, stream_>>>(d_muls_, d_rk + (size_t)160 * byte_stride, d_out,
+                                                                     nb, L);
+    HIPC(hipGetLastError());
+    collect_times();
 }
 
 void Engine::lwe_add(uint64_t *d_a, const uint64_t *d_b, size_t count) {

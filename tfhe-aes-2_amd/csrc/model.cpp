@@ -136,7 +136,7 @@ BitCt Context::trivial(uint64_t bit) const {
     if (bit > 1) throw ModelError{TAE_E_ARG, "cleartext out of bounds: " + std::to_string(bit)};
     BitCt b;
     b.ct.assign(bit_len(), 0);
-    b.ct.back() = encode_bit(bit);
+    b.ct.back() = params().model == 2 ? bit << 62 : encode_bit(bit);  // shortint create_trivial: m * delta
     b.noise = NoiseLevel::trivial();
     b.max_noise_sq = params().max_noise_sq;
     return b;
@@ -145,9 +145,11 @@ BitCt Context::trivial(uint64_t bit) const {
 BitCt Context::wrap(std::vector<uint64_t> ct, uint64_t noise_level_squared) const {
     BitCt b;
     b.ct = std::move(ct);
-    // 8-bit model: shortint NoiseLevel (additive, no component ids; shortint_woppbs_8bit.rs:94-163)
-    b.noise = params().model == 8 ? NoiseLevel{noise_level_squared, {}}
-                                  : NoiseLevel::with_noise_level(noise_level_squared, next_ct_id());
+    // 8-bit model: shortint NoiseLevel (additive, no component ids; shortint_woppbs_8bit.rs:94-163);
+    // shortint_1bit: XOR is unchecked_add (shortint_1bit.rs:109-120), nothing is tracked
+    b.noise = params().model == 8   ? NoiseLevel{noise_level_squared, {}}
+              : params().model == 2 ? NoiseLevel{}
+                                    : NoiseLevel::with_noise_level(noise_level_squared, next_ct_id());
     b.max_noise_sq = params().max_noise_sq;
     return b;
 }
@@ -430,6 +432,10 @@ std::vector<NoiseLevel> sbox_pbs_noise_schedule(const std::vector<NoiseLevel> &r
 std::vector<NoiseLevel> Context::block_noise_schedule(AesDriver driver, const std::vector<NoiseLevel> &rk,
                                                       const std::vector<NoiseLevel> &block, int rounds) const {
     const uint64_t max = params().max_noise_sq;
+    // shortint_1bit: XOR is shortint unchecked_add (shortint_1bit.rs:109-120) and SubBytes a fresh
+    // bootstrap: nothing is validated, so the round function cannot fail on noise bookkeeping (its
+    // decryption failures are the reference's #[ignore]d "too big noise accumulation")
+    if (params().model == 2) return std::vector<NoiseLevel>(128);
     if (params().model == 8) return aes8_noise_schedule(rk, block, rounds, max);
     return driver == AesDriver::SboxPbs ? sbox_pbs_noise_schedule(rk, block, rounds, max)
                                         : aes_noise_schedule(rk, block, rounds, max);
@@ -444,6 +450,10 @@ void Context::run_aes_blocks(AesDriver driver, const uint64_t *d_rk, const uint6
         engine_->aes8_encrypt_blocks(d_rk, d_in, n_blocks, rounds, d_out);
         return;
     }
+    if (params().model == 2) {
+        engine_->s1_aes_encrypt_blocks(d_rk, d_in, n_blocks, rounds, d_out);
+        return;
+    }
     if (driver == AesDriver::SboxPbs && rounds != 1)
         throw ModelError{TAE_E_INDEP, "noise components not independent"};
     engine_->aes_encrypt_blocks(d_rk, d_in, n_blocks, rounds, d_out);
@@ -455,8 +465,8 @@ void Context::aes_encrypt_blocks_raw(const uint64_t *rk, const uint64_t *blocks,
     {
         // static validation of the fixed noise schedule for fresh inputs (noise^2 = 1, own ids)
         std::vector<NoiseLevel> krk(44 * 32), kbl(128);
-        for (auto &x : krk) x = params().model == 8 ? NoiseLevel{1, {}} : NoiseLevel::with_noise_level(1, next_ct_id());
-        for (auto &x : kbl) x = params().model == 8 ? NoiseLevel{1, {}} : NoiseLevel::with_noise_level(1, next_ct_id());
+        for (auto &x : krk) x = params().model != 1 ? NoiseLevel{1, {}} : NoiseLevel::with_noise_level(1, next_ct_id());
+        for (auto &x : kbl) x = params().model != 1 ? NoiseLevel{1, {}} : NoiseLevel::with_noise_level(1, next_ct_id());
         block_noise_schedule(driver, krk, kbl, rounds);
     }
     const size_t S = bit_len();
@@ -524,7 +534,7 @@ std::vector<BitCt> Context::aes_encrypt_blocks(const std::vector<const BitCt *> 
 // (SubWord(RotWord) + Rcon when i%4 == 0), then every bit of word i is bootstrapped (identity LUT).
 std::vector<BitCt> Context::aes_key_schedule(const std::vector<const BitCt *> &key, AesDriver driver) {
     if (key.size() != 128) throw ModelError{TAE_E_ARG, "key must be 16 bytes (128 bits)"};
-    if (params().model == 8 || driver == AesDriver::SboxPbs) return sbox_pbs_key_schedule(key);
+    if (params().model != 1 || driver == AesDriver::SboxPbs) return sbox_pbs_key_schedule(key);
     const size_t L = params().big_len();
     std::vector<BitCt> ek(44 * 32);
     for (int i = 0; i < 128; i++) ek[i] = *key[i];
@@ -590,6 +600,57 @@ std::vector<BitCt> Context::sbox_pbs_key_schedule(const std::vector<const BitCt 
     }
     const Lut sbox = generate_lookup_table(8, 8, ftab_sbox);
     const Lut ident = m8 ? generate_lookup_table(8, 8, ftab_id) : generate_lookup_table(1, 1, ftab_id);
+    if (params().model == 2) {
+        // shortint_1bit ByteT (fhe_impls/shortint_1bit.rs:17-50): sbox_substitute = 8 multivariate functions
+        // of the byte's bits, bootstrap_assign = one PBS per bit with the identity test vector; outputs
+        // are fresh shortint ciphertexts (no bookkeeping: unchecked adds)
+        const Engine &e = *engine_;
+        auto boot = [&](std::vector<BitCt *> bits, bool sbox) {
+            const size_t nbits = bits.size();
+            std::vector<uint64_t> in(nbits * L), out(nbits * L);
+            for (size_t t = 0; t < nbits; t++) std::memcpy(&in[t * L], bits[t]->ct.data(), L * 8);
+            std::lock_guard<std::mutex> g(mu_);
+            hip_check(hipSetDevice(engine_->device()), "hipSetDevice");
+            DevBuf d_in(in.size() * 8), d_out(out.size() * 8);
+            hip_check(hipMemcpyAsync(d_in.p, in.data(), in.size() * 8, hipMemcpyHostToDevice, engine_->stream()), "up");
+            if (sbox)
+                engine_->s1_multivariate(d_in.as<uint64_t>(), nbits / 8, 8, e.s1_sbox_tvs(), 8, d_out.as<uint64_t>());
+            else
+                engine_->s1_bootstrap(d_in.as<uint64_t>(), e.s1_identity_tv(), 1, d_out.as<uint64_t>(), nbits);
+            hip_check(hipMemcpyAsync(out.data(), d_out.p, out.size() * 8, hipMemcpyDeviceToHost, engine_->stream()), "dn");
+            engine_->synchronize();
+            for (size_t t = 0; t < nbits; t++) *bits[t] = wrap(std::vector<uint64_t>(out.begin() + t * L, out.begin() + (t + 1) * L), 0);
+        };
+        auto bit_at = [&](int word, int byte, int bit) -> BitCt & { return ek[(word * 4 + byte) * 8 + bit]; };
+        for (int i = 4; i < 44; i++) {
+            if (i % 4 == 0) {
+                std::vector<BitCt> rot(32);
+                std::vector<BitCt *> rp(32);
+                for (int byte = 0; byte < 4; byte++)
+                    for (int b = 0; b < 8; b++) rot[byte * 8 + b] = bit_at(i - 1, (byte + 1) % 4, b);
+                for (int t = 0; t < 32; t++) rp[t] = &rot[t];
+                boot(rp, true);
+                for (int t = 0; t < 32; t++) {
+                    BitCt v = ek[(i - 4) * 32 + t];
+                    v.xor_assign(rot[t]);
+                    ek[i * 32 + t] = std::move(v);
+                }
+                for (int b = 0; b < 8; b++) ek[i * 32 + b].xor_assign(trivial((kRcon[i / 4] >> (7 - b)) & 1));
+            } else {
+                for (int t = 0; t < 32; t++) {
+                    BitCt v = ek[(i - 4) * 32 + t];
+                    v.xor_assign(ek[(i - 1) * 32 + t]);
+                    ek[i * 32 + t] = std::move(v);
+                }
+            }
+            if (i % 4 == 3) {
+                std::vector<BitCt *> ws(128);
+                for (int t = 0; t < 128; t++) ws[t] = &ek[(i - 3) * 32 + t];
+                boot(ws, false);
+            }
+        }
+        return ek;
+    }
     auto boot = [&](std::vector<BitCt *> bits, const Lut &lut) {  // groups of lut.input_bits, in place
         const int n_in = lut.input_bits;
         const size_t groups = bits.size() / n_in;
@@ -654,6 +715,102 @@ void Context::aes_key_schedule_raw(const uint64_t *key, uint64_t *expanded, bool
         hip_check(hipMemcpy(expanded, he.data(), he.size() * 8, hipMemcpyHostToDevice), "upload expanded key");
     else
         std::memcpy(expanded, he.data(), he.size() * 8);
+}
+
+
+
+// ---------------------------------------------------------------------------------------------
+// shortint_1bit model (src/tfhe/shortint_1bit.rs)
+// ---------------------------------------------------------------------------------------------
+void Context::require_s1() const {
+    if (params().model != 2) throw ModelError{TAE_E_PARAM, "this call belongs to the shortint_1bit parameter set"};
+}
+
+void Context::s1_bootstrap_raw(const uint64_t *in, size_t B, const uint64_t *tvs, size_t n_tv, uint64_t *out,
+                               bool device_mem) {
+    require_s1();
+    if (n_tv < 1) throw ModelError{TAE_E_ARG, "at least one test vector"};
+    const size_t L = bit_len(), G = params().glwe_len();
+    // the test vectors are host arrays, always (like the LUTs of the other models)
+    std::lock_guard<std::mutex> g(mu_);
+    hip_check(hipSetDevice(engine_->device()), "hipSetDevice");
+    DevBuf d_tv(n_tv * G * 8);
+    hip_check(hipMemcpyAsync(d_tv.p, tvs, n_tv * G * 8, hipMemcpyHostToDevice, engine_->stream()), "tv upload");
+    if (device_mem) {
+        engine_->order_after_caller();
+        engine_->s1_bootstrap(in, d_tv.as<uint64_t>(), n_tv, out, B);
+        engine_->synchronize();
+        return;
+    }
+    DevBuf d_in(B * L * 8), d_out(B * L * 8);
+    hip_check(hipMemcpyAsync(d_in.p, in, B * L * 8, hipMemcpyHostToDevice, engine_->stream()), "upload");
+    engine_->s1_bootstrap(d_in.as<uint64_t>(), d_tv.as<uint64_t>(), n_tv, d_out.as<uint64_t>(), B);
+    hip_check(hipMemcpyAsync(out, d_out.p, B * L * 8, hipMemcpyDeviceToHost, engine_->stream()), "download");
+    engine_->synchronize();
+}
+
+void Context::s1_packing_keyswitch_raw(const uint64_t *cts, size_t count, uint64_t *glwe, bool device_mem) {
+    require_s1();
+    if (count < 1 || count > (size_t)params().N) throw ModelError{TAE_E_ARG, "packing keyswitch takes 1..N ciphertexts"};
+    run8(cts, count * bit_len(), glwe, params().glwe_len(), device_mem,
+         [&](const uint64_t *i, uint64_t *o, const uint64_t *) { engine_->s1_pack(i, (int)count, o); }, nullptr);
+}
+
+void Context::s1_test_vectors_from_ciphertexts_raw(const uint64_t *ct0, const uint64_t *ct1, size_t B, uint64_t *tvs,
+                                                   bool device_mem) {
+    require_s1();
+    const size_t L = bit_len(), G = params().glwe_len();
+    std::lock_guard<std::mutex> g(mu_);
+    hip_check(hipSetDevice(engine_->device()), "hipSetDevice");
+    // interleave the pairs (2b, 2b+1) = (ct0[b], ct1[b]) on the device, as the tree levels hold them
+    DevBuf d_pairs(2 * B * L * 8), d_pks(2 * B * G * 8);
+    const auto kind = device_mem ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    if (device_mem) engine_->order_after_caller();
+    hip_check(hipMemcpy2DAsync(d_pairs.p, 2 * L * 8, ct0, L * 8, L * 8, B, kind, engine_->stream()), "pairs");
+    hip_check(hipMemcpy2DAsync(d_pairs.as<uint64_t>() + L, 2 * L * 8, ct1, L * 8, L * 8, B, kind, engine_->stream()),
+              "pairs");
+    engine_->s1_pks(d_pairs.as<uint64_t>(), 2 * B, d_pks.as<uint64_t>());
+    if (device_mem) {
+        engine_->s1_tv_from_pks(d_pks.as<uint64_t>(), B, tvs);
+    } else {
+        DevBuf d_tv(B * G * 8);
+        engine_->s1_tv_from_pks(d_pks.as<uint64_t>(), B, d_tv.as<uint64_t>());
+        hip_check(hipMemcpyAsync(tvs, d_tv.p, B * G * 8, hipMemcpyDeviceToHost, engine_->stream()), "download");
+        engine_->synchronize();
+        return;
+    }
+    engine_->synchronize();
+}
+
+void Context::s1_multivariate_raw(const uint64_t *bits, size_t G, int nbits, const uint64_t *f_tables, int n_fn,
+                                  uint64_t *out, bool device_mem) {
+    require_s1();
+    if (nbits < 1 || nbits > 8) throw ModelError{TAE_E_ARG, "multivariate functions take 1..=8 bits (shortint_1bit.rs:484)"};
+    if (n_fn < 1) throw ModelError{TAE_E_ARG, "at least one function"};
+    const size_t L = bit_len(), GL = params().glwe_len(), V = (size_t)1 << (nbits - 1);
+    // generate_multivariate_test_vector (:478-495): test vector v of function f selects f(2v + bit)
+    std::vector<uint64_t> tvs((size_t)n_fn * V * GL);
+    for (int f = 0; f < n_fn; f++)
+        for (size_t v = 0; v < V; v++) {
+            const uint64_t *tab = f_tables + (size_t)f * 2 * V;
+            if (tab[2 * v] > 1 || tab[2 * v + 1] > 1) throw ModelError{TAE_E_ARG, "function values must be 0 or 1"};
+            s1_test_vector(params(), tab[2 * v], tab[2 * v + 1], &tvs[((size_t)f * V + v) * GL]);
+        }
+    std::lock_guard<std::mutex> g(mu_);
+    hip_check(hipSetDevice(engine_->device()), "hipSetDevice");
+    DevBuf d_tv(tvs.size() * 8);
+    hip_check(hipMemcpyAsync(d_tv.p, tvs.data(), tvs.size() * 8, hipMemcpyHostToDevice, engine_->stream()), "tv upload");
+    if (device_mem) {
+        engine_->order_after_caller();
+        engine_->s1_multivariate(bits, G, nbits, d_tv.as<uint64_t>(), n_fn, out);
+        engine_->synchronize();
+        return;
+    }
+    DevBuf d_in(G * nbits * L * 8), d_out(G * n_fn * L * 8);
+    hip_check(hipMemcpyAsync(d_in.p, bits, G * nbits * L * 8, hipMemcpyHostToDevice, engine_->stream()), "upload");
+    engine_->s1_multivariate(d_in.as<uint64_t>(), G, nbits, d_tv.as<uint64_t>(), n_fn, d_out.as<uint64_t>());
+    hip_check(hipMemcpyAsync(out, d_out.p, G * n_fn * L * 8, hipMemcpyDeviceToHost, engine_->stream()), "download");
+    engine_->synchronize();
 }
 
 }  // namespace tae

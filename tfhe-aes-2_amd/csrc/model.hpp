@@ -91,13 +91,27 @@ class Context {  // FheContext
                               AesDriver driver = AesDriver::GalMul);
 
     // ---- 8-bit model (src/tfhe/shortint_woppbs_8bit.rs, fhe_impls/shortint_woppbs_8bit.rs) ----
-    size_t bit_len() const { return params().model == 8 ? params().small_len() : params().big_len(); }
+    size_t bit_len() const { return params().bit_len(); }
     // FheContext::bootstrap_from_bits over G bytes: bits [G][8][n+1] -> int ciphertexts [G][K+1]
     void bootstrap_from_bits_raw(const uint64_t *bits, size_t groups, const Lut &lut, uint64_t *out, bool device_mem);
     // FheContext::extract_bits_from_ciphertext over G ints: [G][K+1] -> [G][8][n+1]
     void extract_bits_raw(const uint64_t *ints, size_t groups, uint64_t *out, bool device_mem);
 
+    // ---- shortint_1bit model (src/tfhe/shortint_1bit.rs; param set SHORTINT_1BIT), raw arrays ----
+    // FheContext::bootstrap over B bits [B][n+1] with test vectors tvs [n_tv][(k+1)N] (bit b takes b % n_tv)
+    void s1_bootstrap_raw(const uint64_t *in, size_t B, const uint64_t *tvs, size_t n_tv, uint64_t *out, bool device_mem);
+    // FheContext::packing_keyswitch: count bits -> one GLWE [(k+1)N]
+    void s1_packing_keyswitch_raw(const uint64_t *cts, size_t count, uint64_t *glwe, bool device_mem);
+    // test_vector_from_ciphertexts over B pairs (ct0[b], ct1[b]) -> [B][(k+1)N]
+    void s1_test_vectors_from_ciphertexts_raw(const uint64_t *ct0, const uint64_t *ct1, size_t B, uint64_t *tvs,
+                                              bool device_mem);
+    // calculate_multivariate_function for n_fn functions (f_tables [n_fn][2^nbits], host, 0/1 values) of
+    // G groups of nbits bits [G][nbits][n+1] -> [G][n_fn][n+1]
+    void s1_multivariate_raw(const uint64_t *bits, size_t G, int nbits, const uint64_t *f_tables, int n_fn,
+                             uint64_t *out, bool device_mem);
+
   private:
+    void require_s1() const;
     template <class F>
     void run8(const uint64_t *in, size_t in_len, uint64_t *out, size_t out_len, bool device_mem, F fn, const Lut *lut);
     std::vector<BitCt> sbox_pbs_key_schedule(const std::vector<const BitCt *> &key);

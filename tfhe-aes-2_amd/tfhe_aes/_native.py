@@ -17,6 +17,7 @@ TAE_MEM_HOST, TAE_MEM_DEVICE = 0, 1
 TAE_INDEX_AUTO = 2**64 - 1  # tae_encrypt_*_raw: reserve fresh encryption indices from the key's counter
 PARAMS_SQRD_LVL_1, PARAMS_SQRD_LVL_4, PARAMS_SQRD_LVL_64, PARAMS_SQRD_LVL_256 = 0, 1, 2, 3
 PARAMS_WOPPBS_8BIT = 4  # shortint_woppbs_8bit.rs:39-86 (bits under the small key)
+PARAMS_SHORTINT_1BIT = 5  # shortint_1bit.rs:62-83 (shortint bits under the small key, classic PBS)
 
 # Every symbol include/tfhe_aes_gpu.h declares (checked by tests/test_capi_symbols.py).
 EXPORTED = [
@@ -35,6 +36,8 @@ EXPORTED = [
     "tae_last_stage_times_v3", "tae_generate_multivariate_luts", "tae_xor_batch",
     "tae_aes_sbox_pbs_encrypt_blocks", "tae_aes_sbox_pbs_key_schedule", "tae_aes_sbox_pbs_encrypt_blocks_raw",
     "tae_aes_sbox_pbs_key_schedule_raw", "tae_aes_noise_schedule_check",
+    "tae_s1_test_vector_from_fn", "tae_s1_bootstrap", "tae_s1_packing_keyswitch",
+    "tae_s1_test_vectors_from_ciphertexts", "tae_s1_multivariate",
 ]
 TAE_DRIVER_GAL_MUL, TAE_DRIVER_SBOX_PBS = 0, 1
 TAE_KEYS_CLIENT, TAE_KEYS_SERVER = 1, 2
@@ -136,6 +139,11 @@ def lib() -> C.CDLL:
         "tae_keys_save": ([C.c_char_p, C.c_int, vp, vp, vp, vp], C.c_int),
         "tae_keys_file_info": ([C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int)], C.c_int),
         "tae_keys_load": ([C.c_char_p, vpp, vp, vp, vp], C.c_int),
+        "tae_s1_test_vector_from_fn": ([C.c_int, u64, u64, vp], C.c_int),
+        "tae_s1_bootstrap": ([vp, vp, sz, vp, sz, vp, C.c_int], C.c_int),
+        "tae_s1_packing_keyswitch": ([vp, vp, sz, vp, C.c_int], C.c_int),
+        "tae_s1_test_vectors_from_ciphertexts": ([vp, vp, vp, sz, vp, C.c_int], C.c_int),
+        "tae_s1_multivariate": ([vp, vp, sz, C.c_int, vp, C.c_int, vp, C.c_int], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -230,6 +230,18 @@ class ShortintWoppbs8BitSboxPbsAesEncrypt(ShortintWoppbs1BitSboxPbsAesEncrypt):
     """
 
 
+class Shortint1BitSboxPbsAesEncrypt(ShortintWoppbs1BitSboxPbsAesEncrypt):
+    """fhe_impls/shortint_1bit.rs:52-72 -- the fhe_sbox_pbs driver over the shortint_1bit model.
+
+    Same API; use a context of param set PARAMS_SHORTINT_1BIT (bits are shortint ciphertexts under the small
+    key [n+1]).  ByteT::sbox_substitute is 8 multivariate functions of the byte (one selector tree per output
+    bit, :32-50), bootstrap_assign one PBS per bit with the identity test vector (:18-30); XOR is unchecked
+    addition, so nothing raises.  The reference #[ignore]s its AES tests with these testing parameters ("tests
+    fail currently due to too big noise accumulation", :79-102): decryptions of whole rounds may be wrong, as
+    there.  The C-ABI dispatches on the model.
+    """
+
+
 def noise_schedule_check(param_set: int, driver: int, rounds: int) -> None:
     """The round function's noise bookkeeping for fresh inputs, without a context or device: raises the
     error the reference panics with (NoiseNotIndependent / NoiseTooBig), else returns None."""
