@@ -29,13 +29,15 @@
 namespace tae {
 namespace br512lat {
 
-using br512::BUF_STRIDE;
+using br512x4::BUF_STRIDE;  // br512x4's bank-conflict-free spectrum layout (sidx), with the raw inverse
+using br512x4::SF;          // outputs of I1 at natural index j < 256 in the same 290-slot regions
+using br512x4::SG1;
+using br512x4::SG3;
+using br512x4::sidx;
 using br512::K1;
 using br512::lds_sync;
 using br512::M;
-using br512::mac_pos;
 using br512::N;
-using br512::pidx;
 using br512::u32x4;
 using br512::wave_sync;
 using br512x4::dft16x4;
@@ -109,7 +111,8 @@ __global__ void __launch_bounds__(THREADS, 1)
     const uint32_t gbytes = (uint32_t)((size_t)n * ggsw_sz * sizeof(cplx));
     const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc((void *)bsk, (short)0, gbytes, 0x00020000);
     // MAC chains: thread tid runs chain (q = tid >> 8, pos); threads tid < 256 also run (q = 4, pos)
-    const int pos = mac_pos(tid & (M - 1)), qa = tid >> 8;
+    const int pos = tid & (M - 1), qa = tid >> 8, spos = sidx(pos);
+    const int baseA = SF[4 * (u & 3) + r] + SG1[u >> 2], baseB = SF[4 * r + (u & 3)] + SG3[u >> 2];
     const bool two = tid < M;
     const int goff = pos * (int)sizeof(cplx);
     const cplx *my_w16 = s_w16 + 3 * r;
@@ -191,15 +194,15 @@ __global__ void __launch_bounds__(THREADS, 1)
 #pragma unroll
             for (int k2 = 0; k2 < 4; k2++) {
                 const int kq = r + 4 * k2;
-                dst[pidx(u + 16 * kq)] = cmul(v[k2], s_twa[16 * kq + u]);
+                dst[baseA + SG3[k2]] = cmul(v[k2], s_twa[16 * kq + u]);
             }
             wave_sync();
             // pass B (row u): DFT16 over positions 16 u + r + 4 i, in place
 #pragma unroll
-            for (int i = 0; i < 4; i++) v[i] = dst[pidx(16 * u + r + 4 * i)];
+            for (int i = 0; i < 4; i++) v[i] = dst[baseB + SG1[i]];
             dft16x4<false>(v, w16);
 #pragma unroll
-            for (int k2 = 0; k2 < 4; k2++) dst[pidx(16 * u + r + 4 * k2)] = v[k2];
+            for (int k2 = 0; k2 < 4; k2++) dst[baseB + SG1[k2]] = v[k2];
         }
         LPROF(2);
         lds_sync();
@@ -221,7 +224,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                 }
 #pragma unroll
                 for (int p = 0; p < K1; p++) {
-                    const cplx x = buf[((lev - 1) * K1 + p) * BUF_STRIDE + pidx(pos)];
+                    const cplx x = buf[((lev - 1) * K1 + p) * BUF_STRIDE + spos];
                     ar = fma(x.re, ga[p].re, ar);
                     ar = fma(-x.im, ga[p].im, ar);
                     ai = fma(x.re, ga[p].im, ai);
@@ -234,8 +237,8 @@ __global__ void __launch_bounds__(THREADS, 1)
                     }
                 }
             }
-            obuf[qa * BUF_STRIDE + pidx(pos)] = cplx{ar, ai};
-            if (two) obuf[(K1 - 1) * BUF_STRIDE + pidx(pos)] = cplx{br, bi};
+            obuf[qa * BUF_STRIDE + spos] = cplx{ar, ai};
+            if (two) obuf[(K1 - 1) * BUF_STRIDE + spos] = cplx{br, bi};
         }
         LPROF(4);
         lds_sync();
@@ -249,15 +252,15 @@ __global__ void __launch_bounds__(THREADS, 1)
             for (int k = 0; k < 3; k++) w16[k] = my_w16[k];
             cplx v[4];
 #pragma unroll
-            for (int i = 0; i < 4; i++) v[i] = base[pidx(16 * u + r + 4 * i)];
+            for (int i = 0; i < 4; i++) v[i] = base[baseB + SG1[i]];
             dft16x4<true>(v, w16);
 #pragma unroll
-            for (int k2 = 0; k2 < 4; k2++) base[pidx(16 * u + r + 4 * k2)] = v[k2];
+            for (int k2 = 0; k2 < 4; k2++) base[baseB + SG1[k2]] = v[k2];
             wave_sync();
 #pragma unroll
             for (int i = 0; i < 4; i++) {
                 const int kk = r + 4 * i;
-                v[i] = cmul(base[pidx(u + 16 * kk)], cconj(s_twa[16 * kk + u]));
+                v[i] = cmul(base[baseA + SG3[i]], cconj(s_twa[16 * kk + u]));
             }
             dft16x4<true>(v, w16);
             wave_sync();  // this wave's reads of base precede its writes below (LDS executes in order)
