@@ -82,6 +82,22 @@ __device__ __forceinline__ void body(double *d, unsigned *u, unsigned long long 
 #define F(i) asm volatile("v_mul_f64 %0, %0, %1" : "+v"(d[i]) : "v"(d[(i + 1) & 7]));
         REP8(F) REP8(F)
 #undef F
+    } else if constexpr (CLS == 19) {  // v_fma_f64, each followed by one SALU op (counted: the f64 ops only)
+#define F(i) asm volatile("v_fma_f64 %0, %0, %1, %2\n\ts_add_u32 s20, s20, 1" : "+v"(d[i]) : "v"(d[(i + 1) & 7]), "v"(d[(i + 2) & 7]) : "s20", "scc");
+        REP8(F) REP8(F)
+#undef F
+    } else if constexpr (CLS == 20) {  // v_fma_f64, each followed by two SALU ops
+#define F(i) asm volatile("v_fma_f64 %0, %0, %1, %2\n\ts_add_u32 s20, s20, 1\n\ts_add_u32 s21, s21, 1" : "+v"(d[i]) : "v"(d[(i + 1) & 7]), "v"(d[(i + 2) & 7]) : "s20", "s21", "scc");
+        REP8(F) REP8(F)
+#undef F
+    } else if constexpr (CLS == 21) {  // v_fma_f64, each followed by one s_waitcnt (nothing outstanding)
+#define F(i) asm volatile("v_fma_f64 %0, %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "+v"(d[i]) : "v"(d[(i + 1) & 7]), "v"(d[(i + 2) & 7]));
+        REP8(F) REP8(F)
+#undef F
+    } else if constexpr (CLS == 22) {  // v_fma_f64, each followed by one s_setprio
+#define F(i) asm volatile("v_fma_f64 %0, %0, %1, %2\n\ts_setprio 1" : "+v"(d[i]) : "v"(d[(i + 1) & 7]), "v"(d[(i + 2) & 7]));
+        REP8(F) REP8(F)
+#undef F
     } else if constexpr (CLS == 11) {  // v_pk_fma_f32
 #define F(i) asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(q[i]) : "v"(q[(i + 1) & 7]), "v"(q[(i + 2) & 7]));
         REP8(F) REP8(F)
@@ -92,6 +108,9 @@ __device__ __forceinline__ void body(double *d, unsigned *u, unsigned long long 
 // MIX: class A on waves 0..7, class B on waves 8..15 (two of each per SIMD)
 template <int A, int B, int T = 1024>
 __global__ void __launch_bounds__(T, 1) k(double *out, int iters) {
+    __shared__ double sm[2048];  // 16 KiB: the LDS class reads addresses below 0x4000
+    if (iters < 0) sm[threadIdx.x & 2047] = 1.0;
+    if (iters < -1) out[0] = sm[5];
     double d[8];
     unsigned u[8];
     unsigned long long q[8];
@@ -131,7 +150,8 @@ float run(double *d, int blocks, int iters) {
 static const char *names[] = {"v_fma_f64", "v_add_u32", "v_lshlrev_b64", "v_permlane32_swap", "v_add_f64",
                               "v_pk_add_u16", "v_cvt_f64_i32", "v_mul_lo_u32", "v_lshl_add_u64", "v_cndmask_b32",
                               "v_mov_b32", "v_pk_fma_f32", "fma_f64 dep1", "v_mov_dpp", "cndmask_sgpr", "fma_f64 dep2",
-                              "v_cndmask_dpp", "v_permlane16_swap", "v_mul_f64"};
+                              "v_cndmask_dpp", "v_permlane16_swap", "v_mul_f64", "fma_f64+salu", "fma_f64+2salu",
+                              "fma_f64+s_waitcnt", "fma_f64+s_setprio"};
 
 template <int A, int B, int T = 1024>
 void report(double *d, int blocks, int iters, double ghz) {
@@ -193,5 +213,11 @@ int main() {
     report<18, 18, 1024>(d, cus, iters, ghz);
     report<0, 16, 1024>(d, cus, iters, ghz);
     report<0, 17, 1024>(d, cus, iters, ghz);
+    // does a wave's non-VALU instruction cost VALU issue? (cycles per f64 instruction)
+    report<19, 19, 1024>(d, cus, iters, ghz);
+    report<20, 20, 1024>(d, cus, iters, ghz);
+    report<21, 21, 1024>(d, cus, iters, ghz);
+    report<22, 22, 1024>(d, cus, iters, ghz);
+    report<19, 19, 256>(d, cus, iters, ghz);
     return 0;
 }
