@@ -50,9 +50,10 @@ extern "C" {
 #define TAE_PARAMS_SHORTINT_1BIT 5
 
 /* memory kinds for the raw-array entry points.  TAE_MEM_DEVICE: pointers into the context's device
- * memory.  The library orders itself after all work already queued on that device (it synchronizes
- * the device before its first read of caller buffers, e.g. after an RCCL broadcast or torch copies
- * on other streams), and device outputs are complete when the call returns. */
+ * memory.  By default the library orders itself after all work already queued on that device (it
+ * synchronizes the device before its first read of caller buffers, e.g. after an RCCL broadcast or torch
+ * copies on other streams); after tae_set_caller_stream it waits only for the work queued on that one
+ * stream (an event, no host sync).  Device outputs are complete when the call returns. */
 #define TAE_MEM_HOST 0
 #define TAE_MEM_DEVICE 1
 
@@ -255,6 +256,9 @@ int tae_stage_vertical_packing(const tae_context *ctx, const double *ggsw_f, siz
 
 /* ---- device utilities -------------------------------------------------------------------- */
 int tae_synchronize(const tae_context *ctx);
+/* TAE_MEM_DEVICE inputs are produced on `stream` (a hipStream_t of the context's device, e.g. torch's
+ * current stream); NULL restores the device-wide synchronize.  Not thread-safe against calls in flight. */
+int tae_set_caller_stream(tae_context *ctx, void *stream);
 int tae_set_timing(const tae_context *ctx, int on);
 /* per-stage ms of the last batched call: [keyswitch, pbs, pfks, ggsw_fft, vp] */
 int tae_last_stage_times(const tae_context *ctx, float *ms5);

@@ -92,3 +92,30 @@ def test_xor_batch_state(gpu_context, client):
     with pytest.raises(tfhe_aes.NoiseTooBig):
         gpu_context.xor_batch(a, b, np.full(128, 60, np.uint64), np.full(128, 5, np.uint64))
     assert np.array_equal(a, before)
+
+
+def test_caller_stream_ordering(gpu_context, oracle_keys, client):
+    """tae_set_caller_stream: a TAE_MEM_DEVICE call orders itself after the work queued on the caller's
+    stream only (an event, no device-wide synchronize).  The input is produced by a non-blocking copy
+    and an in-place fix-up on a torch side stream right before the call; the keyswitch output must equal
+    the oracle's.  None restores the default."""
+    torch = pytest.importorskip("torch")
+    n = 6
+    cts = client.encrypt_bits_raw([1, 0, 1, 1, 0, 1], start_index=1 << 31)
+    side = torch.cuda.Stream()
+    h = torch.from_numpy(cts.view(np.int64)).pin_memory()
+    d_in = torch.zeros((n, BIG), dtype=torch.int64, device="cuda")
+    d_out = torch.full((n, 678), -1, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    try:
+        gpu_context.set_caller_stream(side)
+        with torch.cuda.stream(side):
+            d_in.copy_(h, non_blocking=True)
+            d_in.add_(0)  # more work on the same stream
+        N.check(N.lib().tae_stage_keyswitch(gpu_context._h, C.c_void_p(d_in.data_ptr()), n,
+                                            C.c_void_p(d_out.data_ptr()), N.TAE_MEM_DEVICE))
+    finally:
+        gpu_context.set_caller_stream(None)
+    out = d_out.cpu().numpy().view(np.uint64)
+    for i in range(n):
+        assert np.array_equal(out[i], oracle_keys.keyswitch(cts[i])), i

@@ -746,6 +746,14 @@ int tae_synchronize(const tae_context *ctx) {
     });
 }
 
+int tae_set_caller_stream(tae_context *ctx, void *stream) {
+    return guarded([&] {
+        require(ctx, "null");
+        std::lock_guard<std::mutex> g(ctx->ctx->mutex());  // the context's entry points hold the same lock
+        ctx->ctx->engine().set_caller_stream((hipStream_t)stream);
+    });
+}
+
 int tae_set_timing(const tae_context *ctx, int on) {
     return guarded([&] {
         require(ctx, "null");

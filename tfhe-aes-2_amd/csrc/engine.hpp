@@ -124,6 +124,9 @@ class Engine {
     // caller (torch's current stream, an RCCL stream): wait for all device work before the engine's
     // non-blocking stream reads them.
     void order_after_caller();
+    // TAE_MEM_DEVICE ordering: nullptr (default) = device-wide synchronize; otherwise the engine stream
+    // waits on an event recorded on this caller stream (no host sync, other streams not waited for)
+    void set_caller_stream(hipStream_t s) { caller_stream_ = s; }
     const StageTimes &last_times() const { return times_; }
     void set_timing(bool on) { timing_ = on; }
 
@@ -146,6 +149,8 @@ class Engine {
     Params p_;
     int device_;
     hipStream_t stream_ = nullptr;
+    hipStream_t caller_stream_ = nullptr;
+    hipEvent_t caller_ev_ = nullptr;
     bool owns_keys_ = false;
     uint64_t *d_ksk_ = nullptr, *d_pfpksk_ = nullptr;
     cplx *d_bsk_f_ = nullptr;

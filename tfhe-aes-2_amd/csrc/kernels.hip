@@ -886,6 +886,7 @@ Engine::~Engine() {
                     (void *)d_s1_id_tv_, (void *)d_s1_in_, (void *)d_s1_out_, (void *)d_s1_pks_, (void *)d_s1_tv_})
         if (q) hipFree(q);
     for (auto &e : ev_pool_) hipEventDestroy(e);
+    if (caller_ev_) hipEventDestroy(caller_ev_);
     hipStreamDestroy(stream_);
 }
 
@@ -893,7 +894,13 @@ void Engine::synchronize() { HIPC(hipStreamSynchronize(stream_)); }
 
 void Engine::order_after_caller() {
     HIPC(hipSetDevice(device_));
-    HIPC(hipDeviceSynchronize());
+    if (!caller_stream_) {
+        HIPC(hipDeviceSynchronize());
+        return;
+    }
+    if (!caller_ev_) HIPC(hipEventCreateWithFlags(&caller_ev_, hipEventDisableTiming));
+    HIPC(hipEventRecord(caller_ev_, caller_stream_));
+    HIPC(hipStreamWaitEvent(stream_, caller_ev_, 0));
 }
 
 void Engine::reserve(size_t bits, size_t outputs) {

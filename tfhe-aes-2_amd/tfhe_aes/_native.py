@@ -30,7 +30,7 @@ EXPORTED = [
     "tae_circuit_bootstrap_raw", "tae_aes_encrypt_block_for_rounds", "tae_aes_encrypt_blocks",
     "tae_aes_key_schedule", "tae_aes_encrypt_blocks_raw", "tae_stage_keyswitch", "tae_stage_pbs_shift_boolean",
     "tae_stage_bootstrap", "tae_stage_pfks_ggsw", "tae_stage_ggsw_fourier", "tae_stage_vertical_packing",
-    "tae_synchronize", "tae_set_timing", "tae_last_stage_times", "tae_bit_len", "tae_encrypt_ints_raw",
+    "tae_synchronize", "tae_set_caller_stream", "tae_set_timing", "tae_last_stage_times", "tae_bit_len", "tae_encrypt_ints_raw",
     "tae_decrypt_ints_raw", "tae_bootstrap_from_bits_raw", "tae_extract_bits_raw", "tae_aes_key_schedule_raw",
     "tae_last_stage_times_v2", "tae_keys_save", "tae_keys_file_info", "tae_keys_load",
     "tae_last_stage_times_v3", "tae_generate_multivariate_luts", "tae_xor_batch",
@@ -125,6 +125,7 @@ def lib() -> C.CDLL:
         "tae_stage_ggsw_fourier": ([vp, vp, sz, vp, C.c_int], C.c_int),
         "tae_stage_vertical_packing": ([vp, vp, sz, C.c_int, vp, C.c_int, vp, C.c_int], C.c_int),
         "tae_synchronize": ([vp], C.c_int), "tae_set_timing": ([vp, C.c_int], C.c_int),
+        "tae_set_caller_stream": ([vp, vp], C.c_int),
         "tae_last_stage_times": ([vp, C.POINTER(C.c_float)], C.c_int),
         "tae_bit_len": ([C.c_int, C.POINTER(sz)], C.c_int),
         "tae_encrypt_ints_raw": ([vp, vp, sz, u64, vp], C.c_int),

@@ -195,6 +195,12 @@ class FheContext:
     def synchronize(self):
         check(lib().tae_synchronize(self._h))
 
+    def set_caller_stream(self, stream):
+        """Order TAE_MEM_DEVICE calls after the work queued on `stream` only (a torch.cuda.Stream, a raw
+        hipStream_t int, or None for the default device-wide synchronize; include/tfhe_aes_gpu.h)."""
+        handle = getattr(stream, "cuda_stream", stream)
+        check(lib().tae_set_caller_stream(self._h, C.c_void_p(handle) if handle else None))
+
     def set_timing(self, on: bool):
         check(lib().tae_set_timing(self._h, 1 if on else 0))
 
