@@ -46,7 +46,7 @@ extern "C" {
 /* the shortint_1bit model's set: src/tfhe/shortint_1bit.rs:62-83 (ClassicPBSParameters, message modulus 2,
  * carry 1, EncryptionKeyChoice::Small; Shortint1BitSboxPbsAesEncrypt, fhe_impls/shortint_1bit.rs:52-72).
  * Bits are shortint ciphertexts under the SMALL key ([n+1] u64, plaintext m * 2^62); the third server key
- * array ("pfpksk") holds the packing keyswitch key [n][ks_l][(k+1)N] (shortint_1bit.rs:186-196). */
+ * array ("pfpksk") holds the packing keyswitch key [n][ks_l][(k+1)N] (shortint_1bit.rs:176-186). */
 #define TAE_PARAMS_SHORTINT_1BIT 5
 
 /* memory kinds for the raw-array entry points.  TAE_MEM_DEVICE: pointers into the context's device
@@ -184,17 +184,17 @@ int tae_extract_bits_raw(const tae_context *ctx, const uint64_t *ints, size_t gr
 
 /* ---- shortint_1bit model (context of TAE_PARAMS_SHORTINT_1BIT; src/tfhe/shortint_1bit.rs) -------------- */
 /* Test vectors are GLWE ciphertexts [(k+1)N] u64 and always host arrays; bits are [n+1] (mem applies). */
-/* FheContext::test_vector_from_cleartext_fn (:301-314, :349-373) for f(0) = f0, f(1) = f1 */
+/* FheContext::test_vector_from_cleartext_fn (:208-223, :365-390) for f(0) = f0, f(1) = f1 */
 int tae_s1_test_vector_from_fn(int param_set, uint64_t f0, uint64_t f1, uint64_t *tv);
-/* FheContext::bootstrap (:250-286) over count bits: bit b is bootstrapped with tvs[b % n_tv] */
+/* FheContext::bootstrap (:257-294, :296-350) over count bits: bit b is bootstrapped with tvs[b % n_tv] */
 int tae_s1_bootstrap(const tae_context *ctx, const uint64_t *in, size_t count, const uint64_t *tvs, size_t n_tv,
                      uint64_t *out, int mem);
-/* FheContext::packing_keyswitch (:234-248): count (1..N) bits -> one GLWE, bit j at coefficient j */
+/* FheContext::packing_keyswitch (:240-255, :494-518): count (1..N) bits -> one GLWE, bit j at coefficient j */
 int tae_s1_packing_keyswitch(const tae_context *ctx, const uint64_t *cts, size_t count, uint64_t *glwe, int mem);
-/* FheContext::test_vector_from_ciphertexts (:316-332, :375-466) for count pairs: tvs [count][(k+1)N] (mem) */
+/* FheContext::test_vector_from_ciphertexts (:225-238, :392-492) for count pairs: tvs [count][(k+1)N] (mem) */
 int tae_s1_test_vectors_from_ciphertexts(const tae_context *ctx, const uint64_t *ct0, const uint64_t *ct1, size_t count,
                                          uint64_t *tvs, int mem);
-/* calculate_multivariate_function (:497-536) with generate_multivariate_test_vector (:478-495) for n_fn
+/* calculate_multivariate_function (:539-583) with generate_multivariate_test_vector (:520-537) for n_fn
  * functions f_tables [n_fn][2^nbits] (host, 0/1, index = bits MSB first) of each of `groups` groups of
  * nbits (1..8) bits [groups][nbits][n+1] -> out [groups][n_fn][n+1] (ByteT::sbox_substitute is 8
  * functions of a byte, fhe_impls/shortint_1bit.rs:32-50) */

@@ -548,7 +548,7 @@ static void *kg_worker(void *arg) {
         glwe_encrypt(J->glwe_sk, k, N, msg, p->glwe_std, J->seed, P_BSK, c, J->bsk + c * glwe);
     }
     if (p->model == 2) {
-        /* shortint_1bit: lwe_packing_keyswitch_key_generation (shortint_1bit.rs:186-196): input key
+        /* shortint_1bit: lwe_packing_keyswitch_key_generation (shortint_1bit.rs:176-186): input key
          * element i, level l: GLWE encryption of the constant polynomial s_i * 2^(64 - B l) */
         for (size_t c = J->tid; c < (size_t)n * p->pfks_l; c += J->nthreads) {
             size_t i = c / p->pfks_l;
@@ -1354,7 +1354,7 @@ uint64_t or_s1_decrypt(const or_client_key *ck, const uint64_t *ct) {
     return ((x + rounding) >> 62) & 1;
 }
 
-/* test_vector_from_cleartext_fn (shortint_1bit.rs:349-373): body[0..N/2) = encode(f(0)),
+/* test_vector_from_cleartext_fn (shortint_1bit.rs:365-390): body[0..N/2) = encode(f(0)),
  * body[N/2..N) = encode(f(1)), encode_bit = m << 62 (:339-343), then rotate_left(N/4) */
 void or_s1_tv_from_fn(int k, int N, uint64_t f0, uint64_t f1, uint64_t *glwe) {
     memset(glwe, 0, sizeof(uint64_t) * (size_t)(k + 1) * N);
@@ -1412,7 +1412,7 @@ void or_s1_pack(const or_server_key *sk, const uint64_t *cts, int count, uint64_
     free(buf);
 }
 
-/* test_vector_from_ciphertexts (shortint_1bit.rs:375-466), step by step as the reference writes it:
+/* test_vector_from_ciphertexts (shortint_1bit.rs:392-492), step by step as the reference writes it:
  * ct0 fills coefficients [0, N/4) and [3N/4, N), ct1 fills [N/4, 3N/4) */
 void or_s1_tv_from_cts(const or_server_key *sk, const uint64_t *ct0, const uint64_t *ct1, uint64_t *tv) {
     const or_params *p = &sk->p;
@@ -1439,7 +1439,7 @@ void or_s1_tv_from_cts(const or_server_key *sk, const uint64_t *ct0, const uint6
     free(buf);
 }
 
-/* FheContext::bootstrap_assign (shortint_1bit.rs:257-286): apply_programmable_bootstrap (blind
+/* FheContext::bootstrap_assign (shortint_1bit.rs:264-294): apply_programmable_bootstrap (blind
  * rotation of the test vector, sample extraction) then keyswitch_lwe_ciphertext to the small key */
 void or_s1_bootstrap(const or_server_key *sk, const uint64_t *in, const uint64_t *tv, uint64_t *out) {
     const or_params *p = &sk->p;

@@ -21,7 +21,7 @@ def okeys(oracle_mod):
 
 
 def dec_plain(x: int) -> int:
-    """decode_bit (shortint_1bit.rs:345-351): closest multiple of 2^62, then bit 62"""
+    """decode_bit (shortint_1bit.rs:359-364): closest multiple of 2^62, then bit 62"""
     return (((int(x) + (1 << 61)) >> 62) & 1)
 
 

@@ -225,7 +225,7 @@ void generate_keys(const Params &p, const uint8_t seed[32], int threads, ClientK
         glwe_encrypt(seed, BSK, c, S, k, N, msg.data(), p.glwe_std, sk.bsk.data() + c * glwe);
     });
     if (p.model == 2) {
-        // shortint_1bit: lwe_packing_keyswitch_key_generation (shortint_1bit.rs:186-196): input key
+        // shortint_1bit: lwe_packing_keyswitch_key_generation (shortint_1bit.rs:176-186): input key
         // element i, level l: GLWE encryption of the constant polynomial s_i * 2^(64 - pfks_b*l)
         parallel_for((size_t)n * p.pfks_l, threads, [&](size_t c) {
             std::vector<uint64_t> msg(N, 0);

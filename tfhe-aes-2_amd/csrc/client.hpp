@@ -115,7 +115,7 @@ void generate_lut(int N, int input_bits, int output_bits, const uint64_t *f_tabl
 // shortint_woppbs_8bit.rs:262-265): out[i] = (f(i mod 256) mod 256) << 56, i < max(N, 256)
 void generate_lut_without_padding(int N, const uint64_t *f_table /*[256]*/, uint64_t *out);
 
-// shortint_1bit test_vector_from_cleartext_fn (shortint_1bit.rs:349-373) for f(0) = f0, f(1) = f1:
+// shortint_1bit test_vector_from_cleartext_fn (shortint_1bit.rs:365-390) for f(0) = f0, f(1) = f1:
 // trivial GLWE [(k+1)N], body boxes encode(f0) | encode(f1) (encode_bit = m << 62) rotated left by N/4
 void s1_test_vector(const Params &p, uint64_t f0, uint64_t f1, uint64_t *glwe);
 

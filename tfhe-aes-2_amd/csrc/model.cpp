@@ -146,7 +146,7 @@ BitCt Context::wrap(std::vector<uint64_t> ct, uint64_t noise_level_squared) cons
     BitCt b;
     b.ct = std::move(ct);
     // 8-bit model: shortint NoiseLevel (additive, no component ids; shortint_woppbs_8bit.rs:94-163);
-    // shortint_1bit: XOR is unchecked_add (shortint_1bit.rs:109-120), nothing is tracked
+    // shortint_1bit: XOR is unchecked_add (shortint_1bit.rs:103-116), nothing is tracked
     b.noise = params().model == 8   ? NoiseLevel{noise_level_squared, {}}
               : params().model == 2 ? NoiseLevel{}
                                     : NoiseLevel::with_noise_level(noise_level_squared, next_ct_id());
@@ -432,7 +432,7 @@ std::vector<NoiseLevel> sbox_pbs_noise_schedule(const std::vector<NoiseLevel> &r
 std::vector<NoiseLevel> Context::block_noise_schedule(AesDriver driver, const std::vector<NoiseLevel> &rk,
                                                       const std::vector<NoiseLevel> &block, int rounds) const {
     const uint64_t max = params().max_noise_sq;
-    // shortint_1bit: XOR is shortint unchecked_add (shortint_1bit.rs:109-120) and SubBytes a fresh
+    // shortint_1bit: XOR is shortint unchecked_add (shortint_1bit.rs:103-116) and SubBytes a fresh
     // bootstrap: nothing is validated, so the round function cannot fail on noise bookkeeping (its
     // decryption failures are the reference's #[ignore]d "too big noise accumulation")
     if (params().model == 2) return std::vector<NoiseLevel>(128);
@@ -785,7 +785,7 @@ void Context::s1_test_vectors_from_ciphertexts_raw(const uint64_t *ct0, const ui
 void Context::s1_multivariate_raw(const uint64_t *bits, size_t G, int nbits, const uint64_t *f_tables, int n_fn,
                                   uint64_t *out, bool device_mem) {
     require_s1();
-    if (nbits < 1 || nbits > 8) throw ModelError{TAE_E_ARG, "multivariate functions take 1..=8 bits (shortint_1bit.rs:484)"};
+    if (nbits < 1 || nbits > 8) throw ModelError{TAE_E_ARG, "multivariate functions take 1..=8 bits (shortint_1bit.rs:526)"};
     if (n_fn < 1) throw ModelError{TAE_E_ARG, "at least one function"};
     const size_t L = bit_len(), GL = params().glwe_len(), V = (size_t)1 << (nbits - 1);
     // generate_multivariate_test_vector (:478-495): test vector v of function f selects f(2v + bit)

@@ -114,7 +114,7 @@ class MultivariateTestVector:
 def generate_multivariate_test_vector(ctx: FheContext, bits: int, f: Callable[[int], Cleartext]) -> MultivariateTestVector:
     """generate_multivariate_test_vector (:478-495); f takes the u8 index of the bits (MSB first)."""
     if not 0 < bits <= 8:
-        raise ValueError("0 < bits <= 8 (shortint_1bit.rs:484)")
+        raise ValueError("0 < bits <= 8 (shortint_1bit.rs:526)")
     return MultivariateTestVector(bits, [_clear(f(v)) for v in range(1 << bits)])
 
 
