@@ -5,7 +5,9 @@
 //   2. for EVERY digit of that range, the offset digit splits into limbs in [-128, 127] that
 //      recombine exactly;
 //   3. with random u64 keys, sum_m limb_m (KEY << 8 m) + c KEY == digit KEY (mod 2^64), the identity
-//      the GEMM (pre-shifted key rows) plus the per-column correction rely on.
+//      the GEMM (pre-shifted key rows) plus the per-column correction rely on; on a clamped level the
+//      digit +2^(B-1) is stored as -2^(B-1) and the identity holds with pfks_clamp_fixup's extra
+//      KEY << B term.  Both plans (clamping allowed, the default, and not: TAE_PFKS_LAYOUT=k5).
 // Shapes: the MFMA PFKS sets, base 2^16 x 2 levels (params_sqrd_lvl_4 / _64) and 2^12 x 3 (lvl_256,
 // the 8-bit model).  Usage: kslots_test [random inputs]; prints OK.
 #include <cstdio>
@@ -27,9 +29,9 @@ static int fails = 0;
         }                                      \
     } while (0)
 
-static void run_shape(int base_log, int levels, long n_random) {
+static void run_shape(int base_log, int levels, long n_random, bool clamp) {
     KSlots ks;
-    CHECK(tae::ksgemm::kslots_build(base_log, levels, ks), "plan for 2^%d x %d", base_log, levels);
+    CHECK(tae::ksgemm::kslots_build(base_log, levels, ks, clamp), "plan for 2^%d x %d", base_log, levels);
     CHECK(ks.S <= 8, "S = %d", ks.S);
     const int64_t half = 1ll << (base_log - 1);
     std::mt19937_64 rng(base_log * 131 + levels);
@@ -67,8 +69,11 @@ static void run_shape(int base_log, int levels, long n_random) {
         const int64_t lo = l == 0 ? -half + 1 : -half;
         const int n = ks.nlimb[l];
         for (int64_t digit = lo; digit <= half; digit++) {
-            int64_t d = digit - ks.off[l], back = 0, scale = 1;
-            uint64_t prod = (uint64_t)ks.off[l] * key[l];
+            const bool clamped = ks.clamp[l] && digit == half;
+            CHECK(!ks.clamp[l] || l > 0, "2^%d: the top level is never clamped", base_log);
+            const int64_t stored = clamped ? -half : digit;
+            int64_t d = stored - ks.off[l], back = 0, scale = 1;
+            uint64_t prod = (uint64_t)ks.off[l] * key[l] + (clamped ? key[l] << base_log : 0);
             for (int m = 0; m < n; m++) {
                 const int64_t limb = tae::ksgemm::kl_next_limb(d, m == n - 1);
                 CHECK(limb >= -128 && limb <= 127, "2^%d level %d digit %lld limb %d = %lld", base_log, l + 1,
@@ -77,21 +82,24 @@ static void run_shape(int base_log, int levels, long n_random) {
                 scale *= 256;
                 prod += (uint64_t)limb * (key[l] << (8 * m));
             }
-            CHECK(back == digit - ks.off[l], "2^%d level %d digit %lld recombines to %lld", base_log, l + 1,
+            CHECK(back == stored - ks.off[l], "2^%d level %d digit %lld recombines to %lld", base_log, l + 1,
                   (long long)digit, (long long)(back + ks.off[l]));
             CHECK(prod == (uint64_t)digit * key[l], "2^%d level %d digit %lld: limb products != digit * key",
                   base_log, l + 1, (long long)digit);
         }
     }
-    std::printf("2^%d x %d: S = %d, limbs/level", base_log, levels, ks.S);
-    for (int l = 0; l < levels; l++) std::printf(" %d (c = %lld)", ks.nlimb[l], (long long)ks.off[l]);
+    std::printf("2^%d x %d%s: S = %d, limbs/level", base_log, levels, clamp ? "" : " (no clamp)", ks.S);
+    for (int l = 0; l < levels; l++)
+        std::printf(" %d (c = %lld%s)", ks.nlimb[l], (long long)ks.off[l], ks.clamp[l] ? ", clamped" : "");
     std::printf("\n");
 }
 
 int main(int argc, char **argv) {
     const long n = argc > 1 ? std::atol(argv[1]) : 1000000;
-    run_shape(16, 2, n);
-    run_shape(12, 3, n);
+    for (bool clamp : {true, false}) {
+        run_shape(16, 2, n, clamp);
+        run_shape(12, 3, n, clamp);
+    }
     if (fails) {
         std::printf("%d failures\n", fails);
         return 1;

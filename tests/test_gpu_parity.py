@@ -145,16 +145,19 @@ def _layout_context(product_raw, layout):
 
 @pytest.fixture(scope="module")
 def layout_contexts(product_raw):
-    return {lay: _layout_context(product_raw, lay) for lay in ("k", "rows")}
+    return {lay: _layout_context(product_raw, lay) for lay in ("k", "k5", "rows")}
 
 
-@pytest.mark.parametrize("layout", ["k", "rows"])
+@pytest.mark.parametrize("layout", ["k", "k5", "rows"])
 def test_pfks_gemm_ragged_bit_exact(layout_contexts, oracle_keys, pfks_batch, layout):
-    """The PFKS GEMM (ksgemm::gemm_g6) in both operand layouts -- K layout (5 limb slots per
-    coefficient, 384-ciphertext tiles, digit-offset correction) and 6-bit row-tile limbs (384-row tiles
-    = 128 ciphertexts x 3 limbs) -- on a ragged batch: rows from full and partial M tiles, including
-    the digit-range extremes, equal the oracle's private functional keyswitch (the scalar u64 kernel,
-    used by params_sqrd_lvl_1, is pinned through test_gpu_model8.py::test_other_n1024_sets_bit_exact)."""
+    """The PFKS GEMM (ksgemm::gemm_g6) in every operand layout -- K layout (4 limb slots per
+    coefficient: the lower level's rare +32768 digits stored as -32768 and corrected by
+    ksgemm::pfks_clamp_fixup; 384-ciphertext tiles, digit-offset correction), the same with 5 slots and no
+    clamping ("k5"), and 6-bit row-tile limbs (384-row tiles = 128 ciphertexts x 3 limbs) -- on a ragged
+    batch: rows from full and partial M tiles, including the digit-range extremes (rows 5 and 390 hold
+    ~170 lower digits of +32768 each), equal the oracle's private functional keyswitch (the scalar u64
+    kernel, used by params_sqrd_lvl_1, is pinned through
+    test_gpu_model8.py::test_other_n1024_sets_bit_exact)."""
     ctx = layout_contexts[layout]
     big = pfks_batch
     out = np.zeros((len(big), 5, 5 * 512), dtype=np.uint64)

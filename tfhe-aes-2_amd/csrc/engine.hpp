@@ -198,6 +198,8 @@ class Engine {
     ksgemm::KSlots pf_slots_;
     int8_t *d_pf_bt_kl_ = nullptr;
     uint64_t *d_pf_corr_ = nullptr;  // [ncols] digit-offset correction of the K layout
+    uint32_t *d_pf_flags_ = nullptr;  // [B][words] clamped-digit flags of the K layout (kslots_build)
+    size_t cap_pf_flags_ = 0;
     int8_t *d_pf_bt_ = nullptr, *d_ks_bt_ = nullptr, *d_digits_ = nullptr;
     size_t cap_digits_ = 0;
     int kp_pf_ = 0, kp_ks_ = 0;

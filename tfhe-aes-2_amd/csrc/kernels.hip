@@ -824,10 +824,14 @@ void Engine::prepare_mfma_keys() {
     dim3 gpf((kp_pf_ + 63) / 64, (nc_pf + 63) / 64), gks((kp_ks_ + 63) / 64, (nc_ks + 63) / 64);
     // the LDS-DMA GEMM reads both operands row-pair interleaved (ksgemm::op_off; Kp % 128 == 0)
     ksgemm::prep_key<<<gpf, kThreads, 0, stream_>>>(d_pfpksk_, d_pf_bt_, kd_pf, kp_pf_, nc_pf, glwe, glwe, pf_blk, true);
-    pf_kl_ = ksgemm::kslots_build(p_.pfks_b, p_.pfks_l, pf_slots_);
-    if (const char *lay = getenv("TAE_PFKS_LAYOUT")) {
+    // TAE_PFKS_LAYOUT (a tuning knob, every value pinned by tests/test_gpu_parity.py): "rows" = 6-bit
+    // row-tile limbs always, "k" = K layout always, "k5" = K layout always and without clamped digits
+    const char *lay = getenv("TAE_PFKS_LAYOUT");
+    const bool k5 = lay && !strcmp(lay, "k5");
+    pf_kl_ = ksgemm::kslots_build(p_.pfks_b, p_.pfks_l, pf_slots_, !k5);
+    if (lay) {
         if (!strcmp(lay, "rows")) pf_kl_min_ = LONG_MAX;
-        if (!strcmp(lay, "k")) pf_kl_min_ = 0;
+        if (!strcmp(lay, "k") || k5) pf_kl_min_ = 0;
     }
     if (pf_kl_) {  // K-layout key rows (limbs in K) and the per-column offset correction
         kp_pf_kl_ = ((p_.K() + 1) * pf_slots_.S + ksgemm::TK - 1) / ksgemm::TK * ksgemm::TK;
@@ -883,7 +887,7 @@ Engine::~Engine() {
                     (void *)d_ggsw_f_, (void *)d_state_, (void *)d_muls_, (void *)d_pf_bt_, (void *)d_ks_bt_, (void *)d_pf_corr_, (void *)d_pf_bt_kl_,
                     (void *)d_digits_, (void *)d_wlut_sbox_, (void *)d_wlut_id_, (void *)d_lut_x_, (void *)d_xbuf_,
                     (void *)d_xsh_, (void *)d_xks_, (void *)d_xpbs_, (void *)d_ints_, (void *)d_s1_sbox_tv_,
-                    (void *)d_s1_id_tv_, (void *)d_s1_in_, (void *)d_s1_out_, (void *)d_s1_pks_, (void *)d_s1_tv_})
+                    (void *)d_s1_id_tv_, (void *)d_s1_in_, (void *)d_s1_out_, (void *)d_s1_pks_, (void *)d_s1_tv_, (void *)d_pf_flags_})
         if (q) hipFree(q);
     for (auto &e : ev_pool_) hipEventDestroy(e);
     if (caller_ev_) hipEventDestroy(caller_ev_);
@@ -1009,14 +1013,31 @@ void Engine::pfks_into_ggsw(const uint64_t *d_big, uint64_t *d_ggsw, size_t B, i
         const long mt = (long)((B + 383) / 384);  // 384-ciphertext tiles
         ensure_digits(d_digits_, cap_digits_, (size_t)mt * 384, kd, kp_pf_kl_, stream_, true);
         const size_t thr = B * (size_t)(K + 1);
+        bool clamp = false;
+        for (int l = 0; l < p_.pfks_l; l++) clamp = clamp || pf_slots_.clamp[l];
+        const int fw = (int)(((size_t)(K + 1) * p_.pfks_l + 31) / 32);  // flag words per ciphertext
+        if (clamp) {
+            const size_t need = B * (size_t)fw;
+            if (need > cap_pf_flags_) {
+                if (d_pf_flags_) HIPC(hipFree(d_pf_flags_));
+                HIPC(hipMalloc(&d_pf_flags_, need * 4));
+                cap_pf_flags_ = need;
+            }
+            HIPC(hipMemsetAsync(d_pf_flags_, 0, need * 4, stream_));
+        }
         ksgemm::prep_digits_kl<<<(unsigned)((thr + 255) / 256), 256, 0, stream_>>>(
-            d_big, K + 1, d_digits_, (long)B, K + 1, kp_pf_kl_, p_.pfks_b, p_.pfks_l, pf_slots_);
+            d_big, K + 1, d_digits_, (long)B, K + 1, kp_pf_kl_, p_.pfks_b, p_.pfks_l, pf_slots_, d_pf_flags_, fw);
         const int ncols = (p_.k + 1) * glwe;
         const long out_stride = (long)p_.cbs_l * ncols;
         const long ntiles = ((long)ncols * 8 + ksgemm::BTN - 1) / ksgemm::BTN;
         uint64_t *dst = d_ggsw + (size_t)(level - 1) * ncols;
         ksgemm::gemm_g6<6, 4, true><<<(unsigned)(mt * ntiles), 1024, ksgemm::gemm_g6_lds<4>(), stream_>>>(
             d_digits_, d_pf_bt_kl_, kp_pf_kl_, mt, ncols, dst, out_stride, (long)B, d_pf_corr_);
+        if (clamp) {
+            const long pf_blk = (long)(K + 1) * p_.pfks_l * glwe;
+            ksgemm::pfks_clamp_fixup<<<(unsigned)((B + 3) / 4), 256, 0, stream_>>>(
+                d_pf_flags_, fw, (long)B, p_.pfks_l, p_.pfks_b, d_pfpksk_, ncols, glwe, glwe, pf_blk, dst, out_stride);
+        }
         HIPC(hipGetLastError());
         return;
     }

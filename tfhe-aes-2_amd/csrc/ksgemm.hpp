@@ -300,14 +300,23 @@ __global__ void __launch_bounds__(256) prep_digits3(const uint64_t *__restrict__
 // 6-bit row-tile layout, 17% fewer MFMAs; base 2^12 (8-bit model, lvl_256) needs 2 limbs per level
 // instead of 3.  i32 sums stay exact: 128 * 128 * S (K+1) < 2^31 for every set here.
 // digits in the K layout, row-pair interleaved rows b (op_off): one thread per (b, i)
+// clamp_flags (levels with ks.clamp): bit (i levels + l) of row b's flag words marks a digit +2^(B-1)
+// stored as -2^(B-1); the words of the rows must be zero on entry.
 __global__ void __launch_bounds__(256) prep_digits_kl(const uint64_t *__restrict__ in, long in_stride,
                                                       int8_t *__restrict__ A, long B, int n_in, int Kp, int base_log,
-                                                      int levels, KSlots ks) {
+                                                      int levels, KSlots ks, uint32_t *__restrict__ clamp_flags = nullptr,
+                                                      int flag_words = 0) {
     const long t = (long)blockIdx.x * 256 + threadIdx.x;
     const long b = t / n_in;
     const int i = (int)(t - b * n_in);
     if (b >= B) return;
+    const int64_t half = 1ll << (base_log - 1);
     kl_for_each_digit(in[b * in_stride + i], base_log, levels, [&](int lev, int64_t digit) {
+        if (ks.clamp[lev - 1] && digit == half) {
+            digit = -half;
+            const int bit = i * levels + lev - 1;
+            atomicOr(clamp_flags + b * flag_words + (bit >> 5), 1u << (bit & 31));
+        }
         int64_t d = digit - ks.off[lev - 1];
         const int n = ks.nlimb[lev - 1];
         const long k0 = (long)i * ks.S + ks.first[lev - 1];
@@ -359,6 +368,38 @@ __global__ void __launch_bounds__(256) key_offset_corr(const uint64_t *__restric
         acc += (uint64_t)ks.off[l] * sum;
     }
     corr[col] = acc;
+}
+
+// Correction of the clamped digits (kslots_build): out[b][col] -= KEY[i][l][col] << base_log for every
+// flag set in row b.  One wave per row; rows without flags (all but ~1-2% at 16-bit digits) cost the
+// read of their flag words.  Every (row, col) belongs to one wave: no atomics.
+__global__ void __launch_bounds__(256) pfks_clamp_fixup(const uint32_t *__restrict__ clamp_flags, int flag_words,
+                                                        long B, int levels, int base_log, const uint64_t *__restrict__ key,
+                                                        int ncols, int cols_per_block, long key_kd_stride,
+                                                        long key_blk_stride, uint64_t *__restrict__ out, long out_stride) {
+    const long b = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (b >= B) return;
+    const uint32_t *fl = clamp_flags + b * flag_words;
+    for (int w0 = 0; w0 < flag_words; w0 += 64) {
+        const uint32_t mine = w0 + lane < flag_words ? fl[w0 + lane] : 0u;
+        uint64_t any = __builtin_amdgcn_ballot_w64(mine != 0);
+        while (any) {
+            const int src = (int)__builtin_ctzll(any);
+            any &= any - 1;
+            uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)mine, src);
+            while (word) {
+                const int bit = (w0 + src) * 32 + (int)__builtin_ctz(word);
+                word &= word - 1;
+                const long kd = bit;  // = i * levels + l, the key row of (i, l)
+                for (int col = lane; col < ncols; col += 64) {
+                    const uint64_t kv =
+                        key[kd * key_kd_stride + (long)(col / cols_per_block) * key_blk_stride + col % cols_per_block];
+                    out[b * out_stride + col] -= kv << base_log;
+                }
+            }
+        }
+    }
 }
 
 // ---- gemm_g6: the PFKS GEMM (3-limb digits, LDS-DMA staging) ----

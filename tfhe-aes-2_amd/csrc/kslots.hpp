@@ -20,24 +20,42 @@ struct KSlots {
     int nlimb[4];     // limbs of level l
     int first[4];     // first slot of level l
     int64_t off[4];   // digit offset c_l
+    int clamp[4];     // 1: level l stores its rare digit +2^(B-1) as -2^(B-1) (see kslots_build)
 };
 
-// balanced n-byte range [-128 (256^n - 1) / 255, 127 (256^n - 1) / 255]
-inline bool kslots_build(int base_log, int levels, KSlots &ks) {
+// balanced n-byte range [-128 (256^n - 1) / 255, 127 (256^n - 1) / 255]: the fewest limbs n and the
+// offset c that hold the digits [lo, hi] of a level
+inline bool kslots_fit(int64_t lo, int64_t hi, int &n, int64_t &c) {
+    for (n = 1; n <= 4; n++) {
+        int64_t span = 0;
+        for (int t = 0; t < n; t++) span = span * 256 + 1;  // (256^n - 1) / 255
+        const int64_t mn = -128 * span, mx = 127 * span;
+        c = hi - mx > 0 ? hi - mx : 0;
+        if (lo - c >= mn) return true;
+    }
+    return false;
+}
+
+// The lower levels' balanced digits span [-2^(B-1), 2^(B-1)]: 2^B + 1 values, one more than B bits
+// hold, and +2^(B-1) only comes up when a level's residue is exactly half the base and the carry rule
+// keeps it (probability ~2^-(B+1) per digit).  With clamp allowed, such a level stores that digit as
+// -2^(B-1) whenever this saves a limb (base 2^16: 2 limbs instead of 3, i.e. 4 slots per coefficient
+// instead of 5 for params_sqrd_lvl_64), and the GEMM output is corrected afterwards by
+// -2^B KEY[i][l][col] for every (ciphertext, i, l) it happened to (ksgemm.hpp pfks_clamp_fixup).
+inline bool kslots_build(int base_log, int levels, KSlots &ks, bool allow_clamp = true) {
     if (levels > 4 || base_log > 30) return false;
     ks.S = 0;
     for (int l = 0; l < levels; l++) {
         const int64_t half = 1ll << (base_log - 1);
         const int64_t lo = l == 0 ? -half + 1 : -half, hi = half;  // the top level drops its carry
-        int n = 1;
-        int64_t c = 0;
-        for (;; n++) {
-            if (n > 4) return false;
-            int64_t span = 0;
-            for (int t = 0; t < n; t++) span = span * 256 + 1;  // (256^n - 1) / 255
-            const int64_t mn = -128 * span, mx = 127 * span;
-            c = hi - mx > 0 ? hi - mx : 0;
-            if (lo - c >= mn) break;
+        int n, n2;
+        int64_t c, c2;
+        if (!kslots_fit(lo, hi, n, c)) return false;
+        ks.clamp[l] = 0;
+        if (allow_clamp && l > 0 && kslots_fit(lo, hi - 1, n2, c2) && n2 < n) {
+            n = n2;
+            c = c2;
+            ks.clamp[l] = 1;
         }
         if (ks.S + n > 8) return false;
         ks.nlimb[l] = n;
