@@ -14,10 +14,12 @@ __global__ void __launch_bounds__(512, 1) k(double *out, int iters) {
     const int w = threadIdx.x >> 6;
     const bool A = w < 4;
     // MODE bits: 1 = A runs VALU, 2 = B runs VALU, 4 = A runs MFMA16, 8 = B runs MFMA16,
-    //            16 = B runs MFMA 4x4x4
+    //            16 = B runs MFMA 4x4x4, 32 = A runs u32 VALU, 64 = A runs permlane32 swaps
     const bool valu = (A && (MODE & 1)) || (!A && (MODE & 2));
     const bool mf16 = (A && (MODE & 4)) || (!A && (MODE & 8));
     const bool mf4 = !A && (MODE & 16);
+    const bool ival = A && (MODE & 32);
+    const bool perm = A && (MODE & 64);
     double s = 0;
     if (valu) {
         double a[16];
@@ -26,6 +28,27 @@ __global__ void __launch_bounds__(512, 1) k(double *out, int iters) {
         for (int it = 0; it < iters; it++)
 #pragma unroll
             for (int i = 0; i < 16; i++) a[i] = fma(a[i], b, c);
+        for (int i = 0; i < 16; i++) s += a[i];
+    }
+    if (ival) {  // integer VALU stream (16 independent u32 chains), the decomposition / torus work
+        unsigned a[16];
+        for (int i = 0; i < 16; i++) a[i] = threadIdx.x * 7u + i;
+        const unsigned b = 0x9E3779B9u;
+        for (int it = 0; it < iters; it++)
+#pragma unroll
+            for (int i = 0; i < 16; i++) a[i] = (a[i] ^ b) + (unsigned)it;
+        for (int i = 0; i < 16; i++) s += a[i];
+    }
+    if (perm) {  // the DFT16 transposes (v_permlane32_swap)
+        unsigned a[16];
+        for (int i = 0; i < 16; i++) a[i] = threadIdx.x * 7u + i;
+        for (int it = 0; it < iters; it++)
+#pragma unroll
+            for (int i = 0; i < 16; i += 2) {
+                auto r = __builtin_amdgcn_permlane32_swap(a[i], a[i + 1], false, false);
+                a[i] = r[0];
+                a[i + 1] = r[1];
+            }
         for (int i = 0; i < 16; i++) s += a[i];
     }
     if (mf16) {
@@ -79,6 +102,11 @@ int main() {
     run<8>(d, it, "B mfma16x16x4");
     run<1 | 8>(d, it, "A valu + B mfma16x16x4");
     run<4 | 8>(d, it, "A mfma16 + B mfma16");
+    run<32>(d, it, "A u32 valu");
+    run<32 | 8>(d, it, "A u32 valu + B mfma16x16x4");
+    run<64>(d, it / 2, "A permlane32 (half iters)");
+    run<64 | 8>(d, it / 2, "A permlane32 + B mfma16 (half)");
+    run<8>(d, it / 2, "B mfma16x16x4 (half iters)");
     run<16>(d, it, "B mfma4x4x4");
     run<1 | 16>(d, it, "A valu + B mfma4x4x4");
     return 0;
