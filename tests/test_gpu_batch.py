@@ -53,6 +53,24 @@ def test_full_batch_128_blocks_two_rounds(gpu_context, oracle_keys, client, read
         assert np.array_equal(out[b], ref), b
 
 
+def test_1024_blocks_one_call_one_round(gpu_context, oracle_keys, client, readme_setup):
+    """BASELINE's largest N (1024 counter-mode blocks) in ONE call on one GPU: each CBS launch is
+    1024 x 16 x 8 = 131072 PBS (43691 br512x4 workgroups, the last one holding two ciphertexts: the
+    512-ciphertext remainder is too big for br512lat), 393216 vertical-packing outputs, and every
+    scratch buffer grows to its size at that batch (GGSW scratch ~13 GB).  One round (ARK(rk0) + final
+    round) keeps it cheap; all blocks decrypt to plain AES, the first and last equal the oracle."""
+    key, iv, rk = readme_setup
+    nb = 1024
+    blocks = aes_128.counter_blocks(iv, nb)
+    cts = client.encrypt_bits_raw(aes_128.blocks_to_bits(blocks), start_index=700_000).reshape(nb, 128, BIG)
+    out = E.encrypt_blocks_raw(gpu_context, rk, cts, rounds=1)
+    got = aes_128.bits_to_blocks(client.decrypt_bits_raw(out))
+    assert got == aes_128.expand_key_and_encrypt_blocks(key, blocks, 1)
+    for b in (0, nb - 1):
+        ref = oracle_keys.aes_encrypt_block(rk, cts[b], 1, threads=16)
+        assert np.array_equal(out[b], ref), b
+
+
 def test_configs3_rank7_of_8_shard(oracle_keys, product_raw, client):
     """BASELINE configs[3] (1024 blocks over 8 GPUs) as its LAST rank runs it, on this one GPU: exactly
     what bench.py does on rank 7 of world 8 with 128 blocks per GPU (main.rs:108-115 counters, sharded
