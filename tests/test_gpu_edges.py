@@ -119,3 +119,22 @@ def test_caller_stream_ordering(gpu_context, oracle_keys, client):
     out = d_out.cpu().numpy().view(np.uint64)
     for i in range(n):
         assert np.array_equal(out[i], oracle_keys.keyswitch(cts[i])), i
+
+
+def test_context_shared_across_host_threads(gpu_context, client):
+    """One context used from six host threads at once (the header's promise, and the reference's
+    FheContext: Send + Sync): ctypes drops the GIL, the context's lock serialises the device work, and
+    every thread gets exactly what a sequential call returns (1-3 blocks, one round, distinct inputs)."""
+    from concurrent.futures import ThreadPoolExecutor
+    E = aes_128.ShortintWoppbs1BitSboxGalMulPbsAesEncrypt
+    rk = client.encrypt_bits_raw([(i * 7 + 3) & 1 for i in range(1408)], start_index=2_000_000)
+    jobs = []
+    for t in range(6):
+        nb = 1 + t % 3
+        bits = [(t * 31 + i * 13) >> 2 & 1 for i in range(128 * nb)]
+        jobs.append(client.encrypt_bits_raw(bits, start_index=2_100_000 + 1000 * t).reshape(nb, 128, BIG))
+    seq = [E.encrypt_blocks_raw(gpu_context, rk, cts, rounds=1) for cts in jobs]
+    with ThreadPoolExecutor(max_workers=6) as pool:
+        par = list(pool.map(lambda cts: E.encrypt_blocks_raw(gpu_context, rk, cts, rounds=1), jobs))
+    for t in range(6):
+        assert np.array_equal(par[t], seq[t]), t
