@@ -221,19 +221,18 @@ __global__ void __launch_bounds__(THREADS, 1)
                 const uint64_t v0 = poly[ph], v1 = poly[ph ^ M];
                 const uint64_t p0 = poly[j], p1 = poly[j + M];
                 const uint64_t x0 = (v0 ^ m0) - (p0 + m0), x1 = (v1 ^ m1) - (p1 + m1);
-                uint32_t d0[LEV], d1[LEV];
-                decompose16t<LEV, BLOG>(x0, d0);
-                decompose16t<LEV, BLOG>(x1, d1);
+                // both coefficients at once with 16-bit SIMD ops (fft_device.hpp decompose16p: level l's
+                // digits of x0 / x1 in the low / high half of dp[l])
+                uint32_t dp[LEV];
+                decompose16p<LEV, BLOG>(x0, x1, dp);
                 if constexpr (BYTES) {
 #pragma unroll
-                    for (int w = 0; w < DW; w++) {
-                        uint32_t v = (d0[2 * w] & 0xFF) | ((d1[2 * w] & 0xFF) << 8);
-                        if (2 * w + 1 < LEV) v |= ((d0[2 * w + 1] & 0xFF) << 16) | ((d1[2 * w + 1] & 0xFF) << 24);
-                        dig[w][m] = v;
-                    }
+                    for (int w = 0; w < DW; w++)  // bytes (x0, x1) of level 2w, then of level 2w + 1
+                        dig[w][m] = 2 * w + 1 < LEV ? perm_b32(dp[2 * w + 1], dp[2 * w], 0x06040200u)
+                                                    : perm_b32(dp[2 * w], dp[2 * w], 0x00000200u) & 0xFFFFu;
                 } else {
 #pragma unroll
-                    for (int l = 0; l < LEV; l++) dig[l][m] = d0[l] | (d1[l] << 16);
+                    for (int l = 0; l < LEV; l++) dig[l][m] = dp[l];
                 }
             }
         }
