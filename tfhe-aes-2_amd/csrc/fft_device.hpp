@@ -271,6 +271,19 @@ __host__ __device__ __forceinline__ void decompose16p(uint64_t x0, uint64_t x1, 
         F[0] = perm_b32(a1, a0, 0x05040100u) & MASK;
         F[1] = perm_b32(h1, h0, 0x06050201u) & MASK;
         F[2] = as_u32(as_u16x2(perm_b32(h1, h0, 0x07060302u)) >> (unsigned short)4);
+    } else if constexpr (LEV == 6 && B == 7) {
+        // the 8-bit model's PBS: fields at bits 22 + 7 i; F0 in the low dwords, F1 straddles them, F2..F5
+        // from the high dwords' 16-bit windows at bits 0, 8 and 16 (v_perm), no 64-bit shifts
+        const uint32_t l0 = (uint32_t)X0, l1 = (uint32_t)X1, h0 = (uint32_t)(X0 >> 32), h1 = (uint32_t)(X1 >> 32);
+        const u16x2 s7 = {0x7F, 0x7F};
+        F[0] = as_u32((as_u16x2(perm_b32(l1, l0, 0x07060302u)) >> (unsigned short)6) & s7);
+        F[1] = perm_b32(alignbit_b32(h1, l1, 29), alignbit_b32(h0, l0, 29), 0x05040100u) & MASK;
+        const u16x2 w0 = as_u16x2(perm_b32(h1, h0, 0x05040100u)), w8 = as_u16x2(perm_b32(h1, h0, 0x06050201u)),
+                    w16 = as_u16x2(perm_b32(h1, h0, 0x07060302u));
+        F[2] = as_u32((w0 >> (unsigned short)4) & s7);
+        F[3] = as_u32((w8 >> (unsigned short)3) & s7);
+        F[4] = as_u32((w16 >> (unsigned short)2) & s7);
+        F[5] = as_u32(w16 >> (unsigned short)9);
     } else {
 #pragma unroll
         for (int i = 0; i < LEV; i++)
