@@ -5,8 +5,9 @@ lane (d0, d1), register d2; pass 1: lane (d0, d2), register d1; pass 2: lane (d1
 a slot function sum-separable in the digits, slot(q) = S0[d0] + S1[d1] + S2[d2], keeps every access a
 per-lane base plus an immediate.  Bank model (MI355X_MICROARCH.md LDS table, as x4_banks.py): read b128
 in 4 lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32), bank group = slot mod 16; write b128 in 8
-contiguous 8-lane groups, bank group = slot mod 8.  Prints the current padding's cost and a conflict-free
-table set (searched) with its slot range."""
+contiguous 8-lane groups, bank group = slot mod 8.  Checks the MAC's position permutation (mac_pos) and
+prints the FFT patterns' cost under the current padding; the table search finds no conflict-free
+sum-separable set (b1k_sep_feasibility.c proves it)."""
 import random
 import sys
 
@@ -75,7 +76,35 @@ def search(seed, step1=9, step2=72, slack=8, iters=20000):
     return c, S
 
 
+def mac_pos(tid):
+    """br1024.hpp mac_pos: half-wave h takes runs r = (h mod 8) + 8 j, j in {0, 2, 1, 3} (+4 for h >= 8)"""
+    h, o = tid >> 5, (tid >> 3) & 3
+    j = (4 if h & 8 else 0) + ((o & 1) << 1) + (o >> 1)
+    return 8 * ((h & 7) + 8 * j) + (tid & 7)
+
+
+def mac_check(pos=mac_pos):
+    """(bijective, extra read cycles, extra write cycles) of the MAC's pidx(pos(tid)) = q + q/8 accesses"""
+    P = [pos(t) for t in range(512)]
+    rd = wr = 0
+    for w in range(8):
+        for groups, mod in ((RD, 16), (WR, 8)):
+            for g in groups:
+                cnt = {}
+                for l in g:
+                    q = P[64 * w + l]
+                    b = (q + (q >> 3)) % mod
+                    cnt[b] = cnt.get(b, 0) + 1
+                if mod == 16:
+                    rd += max(cnt.values()) - 1
+                else:
+                    wr += max(cnt.values()) - 1
+    return sorted(P) == list(range(512)), rd, wr
+
+
 if __name__ == "__main__":
+    print("MAC positions, identity: bijective %s, read %d, write %d" % mac_check(lambda t: t))
+    print("MAC positions, mac_pos:  bijective %s, read %d, write %d" % mac_check())
     cur = [[d for d in range(8)], [9 * d for d in range(8)], [72 * d for d in range(8)]]
     print("current q + q/8: cost", cost(cur), "span", span(cur))
     best = None

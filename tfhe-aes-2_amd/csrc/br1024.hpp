@@ -52,6 +52,18 @@ constexpr int ACC_STRIDE = N;          // u64
 
 __device__ __forceinline__ int pidx(int q) { return q + (q >> 3); }
 
+// The MAC thread's Fourier position.  Consecutive positions put 2 lanes of some ds_read_b128 groups on
+// one bank (pidx's +1 per 8 makes a wave's 64 slots fall unevenly on the 16 bank groups).  Instead each
+// half-wave h takes four runs of 8 positions r = s + 8 j with one class s = h mod 8 and j in {0, 2, 1, 3}
+// (+4 for h >= 8): slots 9 r + i then hit every bank group once per 16-lane group (scripts/layout/
+// b1k_banks.py checks it); a run is one 128-byte line of every GGSW row, so the row loads stay whole
+// lines.  A bijection of the 512 positions (the MAC is per position, the results go back by position).
+__device__ __forceinline__ int mac_pos(int tid) {
+    const int h = tid >> 5, o = (tid >> 3) & 3;
+    const int j = (h & 8 ? 4 : 0) + ((o & 1) << 1) + (o >> 1);
+    return 8 * ((h & 7) + 8 * j) + (tid & 7);
+}
+
 // c ? a : b on the two doubles (a struct select here went through scratch memory)
 __device__ __forceinline__ cplx csel(bool c, cplx a, cplx b) { return {c ? a.re : b.re, c ? a.im : b.im}; }
 
@@ -135,7 +147,7 @@ __global__ void __launch_bounds__(THREADS, 1)
     const cplx *gbase = PBS ? ggsw_base : ggsw_base + (size_t)g * n_in * ggsw_sz;
     const uint32_t gbytes = (uint32_t)((size_t)(PBS ? n : n_in) * ggsw_sz * sizeof(cplx));
     const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc((void *)gbase, (short)0, gbytes, 0x00020000);
-    const int pos = tid;  // MAC: Fourier position
+    const int pos = mac_pos(tid);  // MAC: Fourier position
     const int gvoff = pos * (int)sizeof(cplx);
 
     for (int i = tid; i < CJ * N; i += THREADS) {

@@ -120,7 +120,7 @@ __global__ void __launch_bounds__(THREADS, 1)
         // the passes (dozens of them) do not fit beside the FFT state and spill
         int tq = tid;
         asm volatile("" : "+v"(tq));
-        pos = tq & (M - 1);
+        pos = br1024::mac_pos(tq & (M - 1));  // bank-conflict-free MAC reads (br1024.hpp)
         goff = pos * (int)sizeof(cplx);
         // ---- D: rotated difference and its digits, pairs (p, j), (p, j + M) ----
         {
