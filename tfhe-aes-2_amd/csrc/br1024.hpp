@@ -7,8 +7,10 @@
 // through the job's own LDS region (wave-local, no barrier).  The spectra live one decomposition
 // level at a time (pbs_l = 6); the MAC runs with thread = Fourier position (512) over the six
 // (q, ct) accumulators, each GGSW value loaded once for both ciphertexts.  Operation order per
-// output is the oracle's (explicit fma, the u k == 0 twiddles skipped as there), so results are
-// bit-exact.
+// output is the oracle's (explicit fma).  The oracle skips the u k == 0 twiddles; here every lane
+// multiplies, and W^0 = (1, -0) is exact, so at most the sign of a zero differs, which no later
+// operation turns into a different u64 output (from_torus(+-0) = 0): results are bit-exact, and the
+// lane-uniform code drops two selects per twiddle (8-bit CBS launch -3.9%).
 // LDS (126 KB): ACC [C][k+1][N] u64, spectra [C (k+1)][576] cplx (+1 pad per 8: conflict-free
 // b128 accesses at strides 1, 8 and 64), twist / W_512 / untwist tables.
 #pragma once
@@ -296,7 +298,7 @@ __global__ void __launch_bounds__(THREADS, 1)
 #pragma unroll
                 for (int kk = 1; kk < 8; kk++) {
                     const cplx tv = cmul(v[kk], W0_AT(kk));
-                    X[pidx(tt + 64 * kk)] = csel(tt != 0, tv, v[kk]);
+                    X[pidx(tt + 64 * kk)] = tv;  // W^0 = 1 exactly: only the sign of a zero can differ from skipping it
                 }
                 wave_sync();
                 if (lev0 == LEV) s_setprio_c<1>(); else s_setprio_c<2>();
@@ -310,7 +312,7 @@ __global__ void __launch_bounds__(THREADS, 1)
 #pragma unroll
                     for (int kk = 1; kk < 8; kk++) {
                         const cplx tv = cmul(v[kk], W1_AT(kk));
-                        X[pidx(64 * gg + uu + 8 * kk)] = csel(uu != 0, tv, v[kk]);
+                        X[pidx(64 * gg + uu + 8 * kk)] = tv;  // W^0 = 1 exactly: only the sign of a zero can differ from skipping it
                     }
                 }
                 wave_sync();
@@ -378,7 +380,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                 for (int kk = 1; kk < 8; kk++) {
                     const cplx y = Y[pidx(64 * gg + uu + 8 * kk)];
                     const cplx tv = cmul(y, cconj(W1_AT(kk)));
-                    v[kk] = csel(uu != 0, tv, y);
+                    v[kk] = tv;  // W^0 = 1 exactly: only the sign of a zero can differ from skipping it
                 }
                 dft8<true>(v, w81, w83);
 #pragma unroll
@@ -392,7 +394,7 @@ __global__ void __launch_bounds__(THREADS, 1)
             for (int kk = 1; kk < 8; kk++) {
                 const cplx y = Y[pidx(tt + 64 * kk)];
                 const cplx tv = cmul(y, cconj(W0_AT(kk)));
-                v[kk] = csel(tt != 0, tv, y);
+                v[kk] = tv;  // W^0 = 1 exactly: only the sign of a zero can differ from skipping it
             }
             dft8<true>(v, w81, w83);
             uint64_t *poly = acc + jb * ACC_STRIDE;

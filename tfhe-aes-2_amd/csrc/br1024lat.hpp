@@ -180,7 +180,7 @@ __global__ void __launch_bounds__(THREADS, 1)
 #pragma unroll
                 for (int kk = 1; kk < 8; kk++) {
                     const cplx tv = cmul(v[kk], s_w0[(kk - 1) * 64 + t]);
-                    X[pidx(t + 64 * kk)] = csel(t != 0, tv, v[kk]);
+                    X[pidx(t + 64 * kk)] = tv;  // W^0 = 1 exactly: only the sign of a zero can differ from skipping it
                 }
                 wave_sync();
                 // pass 1: points 64 gg + uu + 8 m, w[8 uu kk]
@@ -194,7 +194,7 @@ __global__ void __launch_bounds__(THREADS, 1)
 #pragma unroll
                     for (int kk = 1; kk < 8; kk++) {
                         const cplx tv = cmul(v[kk], s_w1[(kk - 1) * 8 + uu]);
-                        X[pidx(64 * gg + uu + 8 * kk)] = csel(uu != 0, tv, v[kk]);
+                        X[pidx(64 * gg + uu + 8 * kk)] = tv;  // W^0 = 1 exactly: only the sign of a zero can differ from skipping it
                     }
                 }
                 wave_sync();
@@ -269,7 +269,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                 for (int kk = 1; kk < 8; kk++) {
                     const cplx y = Y[pidx(64 * gg + uu + 8 * kk)];
                     const cplx tv = cmul(y, cconj(s_w1[(kk - 1) * 8 + uu]));
-                    v[kk] = csel(uu != 0, tv, y);
+                    v[kk] = tv;  // W^0 = 1 exactly: only the sign of a zero can differ from skipping it
                 }
                 dft8<true>(v, w81, w83);
 #pragma unroll
@@ -281,7 +281,7 @@ __global__ void __launch_bounds__(THREADS, 1)
             for (int kk = 1; kk < 8; kk++) {
                 const cplx y = Y[pidx(t + 64 * kk)];
                 const cplx tv = cmul(y, cconj(s_w0[(kk - 1) * 64 + t]));
-                v[kk] = csel(t != 0, tv, y);
+                v[kk] = tv;  // W^0 = 1 exactly: only the sign of a zero can differ from skipping it
             }
             dft8<true>(v, w81, w83);
             wave_sync();  // this wave's reads of Y precede its writes below (LDS executes in order)
