@@ -31,6 +31,7 @@ README_KEY = bytes.fromhex("76b8e0ada0f13d90405d6ae55386bd28")  # README / main.
 README_IV = bytes.fromhex("bdd219b8a08ded1a")
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (= FP64 matrix) dense peak, spec
+SPEC_CLOCK_GHZ = 2.4      # the clock the spec peaks assume
 FP64_SUSTAINED_TFLOPS = 58.0  # measured sustained v_fma_f64 rate, all CUs (scripts/probes/fp64_peak.hip)
 PBS_KERNELS = {"1bit": "tae::br512x4::br_kernel<3, true, 12>", "8bit": "tae::br1024::br_kernel<6, true, 7>"}
 
@@ -179,6 +180,14 @@ def main():
     ctx.set_timing(False)
     if dist:
         elapsed = D.max_over_ranks(dist, elapsed, f"cuda:{dev}")
+    # effective shader clock of the PBS launches: one more step, right after the timed ones (chip warm),
+    # with in-kernel clock stamps (a diagnostic mode: each stamped launch is read back synchronously)
+    ctx.set_timing(True, clock=True)
+    step()
+    ctx.synchronize()
+    clk = ctx.last_stage_times()
+    ctx.set_timing(False)
+    clock_ghz = clk.get("pbs_clock_ghz")
 
     # ---- correctness gate: decrypt and compare with plain AES (outside the timed region) ----
     out = out_dev.cpu().numpy().view(np.uint64)
@@ -279,7 +288,9 @@ def main():
                         "algorithmic_bytes_per_launch": k_bytes},
                 "sustained": {"peak": FP64_SUSTAINED_TFLOPS, "frac": (tflops / FP64_SUSTAINED_TFLOPS) if tflops else None,
                               "note": "v_fma_f64 rate the chip holds with every CU busy "
-                                      "(scripts/probes/fp64_peak.hip); the spec peak assumes 2.4 GHz"}}
+                                      "(scripts/probes/fp64_peak.hip); the spec peak assumes 2.4 GHz"},
+                "effective_clock_ghz": clock_ghz,
+                "at_clock": at_clock(tflops, clock_ghz)}
     stage_share = {k: v / args.steps for k, v in stage_ms.items() if k not in ("pbs_launches", "pbs_main_cts")}
 
     cpu = None
@@ -311,6 +322,17 @@ def main():
         print(json.dumps(rec), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def at_clock(tflops, ghz):
+    """The FP64 spec peak scaled to the clock the launches actually ran at (the spec assumes 2.4 GHz):
+    what the kernel's cycles reach at that clock, separable from the chip's DVFS give-back."""
+    if not tflops or not ghz:
+        return None
+    peak = FP64_PEAK_TFLOPS * ghz / SPEC_CLOCK_GHZ
+    return {"peak": peak, "frac": tflops / peak,
+            "note": "in-kernel s_memtime / s_memrealtime stamps of the PBS launches of one extra step after the "
+                    "timed ones (median over workgroups, mean over launches; MI355X_MICROARCH.md DVFS give-back)"}
 
 
 def cpu_share():
@@ -357,9 +379,10 @@ def cpu_baseline(raw, ck, threads, model="1bit", rk=None):
                       "extrapolated (blocks independent, same cores)"}
 
 
-def model8_leg(torch, dev, nb, threads):
+def model8_leg(torch, dev, nb, threads, steps=3):
     """BASELINE configs[4] (ShortintWoppbs8BitSboxPbsAesEncrypt, shortint_woppbs_8bit params) on a bounded
-    batch: nb counter blocks, one warm-up and one timed 10-round step, decrypted against plain AES."""
+    batch: nb counter blocks, one warm-up and `steps` timed 10-round steps (mean, with their spread),
+    decrypted against plain AES."""
     import tfhe_aes
     from tfhe_aes import aes_128
     from tfhe_aes import distributed as D
@@ -382,15 +405,20 @@ def model8_leg(torch, dev, nb, threads):
     step = lambda: E8.encrypt_blocks_device(ctx, rk_dev.data_ptr(), blk_dev.data_ptr(), nb, 10, out_dev.data_ptr())
     step()
     ctx.synchronize()
-    t0 = time.time()
+    times = []
+    for _ in range(steps):
+        t0 = time.time()
+        step()
+        ctx.synchronize()
+        times.append(time.time() - t0)
+    dt = sum(times) / len(times)
+    ctx.set_timing(True, clock=True)  # one more step outside the timed ones: where the time goes
     step()
     ctx.synchronize()
-    dt = time.time() - t0
-    ctx.set_timing(True)  # one more step outside the timed one: where the time goes
-    step()
-    ctx.synchronize()
-    stages = {k: (round(v, 1) if isinstance(v, float) else v) for k, v in ctx.last_stage_times().items()
-              if k not in ("pbs_main", "pbs_main_cts")}
+    st = ctx.last_stage_times()
+    clock_ghz = st.get("pbs_clock_ghz")
+    stages = {k: (round(v, 1) if isinstance(v, float) else v) for k, v in st.items()
+              if k not in ("pbs_main", "pbs_main_cts", "pbs_clock_ghz", "pbs_clock_launches")}
     ctx.set_timing(False)
     got = aes_128.bits_to_blocks(ck.decrypt_bits_raw(out_dev.cpu().numpy().view(np.uint64)))
     ek_plain = aes_128.key_schedule_plain(README_KEY)
@@ -405,9 +433,13 @@ def model8_leg(torch, dev, nb, threads):
                     "achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": (tf / FP64_PEAK_TFLOPS) if tf else None, "launches_per_step": launches,
                     "algorithmic_flop_per_launch": flop_launch,
-                    "note": "stage time of the timing step over its PBS launches (HIP events on the engine stream)"}
+                    "avg_launch_ms": pbs_ms / launches if launches else None,
+                    "effective_clock_ghz": clock_ghz, "at_clock": at_clock(tf, clock_ghz),
+                    "note": "stage time of the timing step over its PBS launches (HIP events on the engine stream; "
+                            "that step also carries the clock stamps)"}
     return {"config": f"ShortintWoppbs8BitSboxPbsAesEncrypt, {nb} counter blocks x 10 rounds on 1 GPU "
-                      "(BASELINE configs[4]); 1 warm-up + 1 timed step", "blocks": nb, "s_per_step": dt,
+                      f"(BASELINE configs[4]); 1 warm-up + {steps} timed steps", "blocks": nb, "s_per_step": dt,
+            "s_per_step_each": times, "spread": (max(times) - min(times)) / dt,
             "value": nb / dt, "unit": "blocks/s", "bit_len": L, "setup_s": setup_s, "stage_ms": stages,
             "cbs_pbs_roofline": cbs_roofline, "correct": bool(correct)}
 

@@ -259,6 +259,8 @@ int tae_synchronize(const tae_context *ctx);
 /* TAE_MEM_DEVICE inputs are produced on `stream` (a hipStream_t of the context's device, e.g. torch's
  * current stream); NULL restores the device-wide synchronize.  Not thread-safe against calls in flight. */
 int tae_set_caller_stream(tae_context *ctx, void *stream);
+/* 0 off; 1 per-stage HIP-event times of each batched call; 2 the same plus in-kernel clock stamps of the
+ * throughput blind-rotation launches (a diagnostic mode: every stamped launch is read back synchronously) */
 int tae_set_timing(const tae_context *ctx, int on);
 /* per-stage ms of the last batched call: [keyswitch, pbs, pfks, ggsw_fft, vp] */
 int tae_last_stage_times(const tae_context *ctx, float *ms5);
@@ -267,6 +269,10 @@ int tae_last_stage_times_v2(const tae_context *ctx, float *ms8);
 /* v2's eight values, then the ms and the ciphertext count of the throughput blind-rotation kernel's
  * own launches (br512x4, without the small-batch remainder) -- the roofline's launch duration */
 int tae_last_stage_times_v3(const tae_context *ctx, double *v10);
+/* v3's ten values, then (timing mode 2) the effective shader clock in GHz of the throughput blind-rotation
+ * launches (median over each launch's workgroups of shader cycles / 100 MHz reference ticks, averaged over
+ * the launches; MI355X_MICROARCH.md "DVFS give-back") and the number of launches it averages (0: none) */
+int tae_last_stage_times_v4(const tae_context *ctx, double *v12);
 
 #ifdef __cplusplus
 }

@@ -1449,8 +1449,8 @@ void or_s1_bootstrap(const or_server_key *sk, const uint64_t *in, const uint64_t
     free(big);
 }
 
-/* generate_multivariate_test_vector (:478-495) + calculate_multivariate_function / apply_selectors_rec
- * (:497-536): the last bit selects inside each test vector, the results are packed pairwise into the
+/* generate_multivariate_test_vector (:519-536) + calculate_multivariate_function / apply_selectors_rec
+ * (:538-576): the last bit selects inside each test vector, the results are packed pairwise into the
  * next level's test vectors (test_vector_from_ciphertexts), the next-to-last bit selects among those... */
 void or_s1_multivariate(const or_server_key *sk, const uint64_t *bits, int nbits, const uint64_t *f_table,
                         uint64_t *out) {

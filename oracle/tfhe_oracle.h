@@ -173,14 +173,14 @@ uint64_t or_s1_decrypt(const or_client_key *ck, const uint64_t *ct);
 void or_s1_tv_from_fn(int k, int N, uint64_t f0, uint64_t f1, uint64_t *glwe);
 /* keyswitch_lwe_ciphertext_into_glwe_ciphertext with the packing keyswitch key: [n+1] -> [(k+1)N] */
 void or_s1_pks(const or_server_key *sk, const uint64_t *in, uint64_t *glwe);
-/* keyswitch_lwe_ciphertext_list_and_pack_in_glwe_ciphertext (FheContext::packing_keyswitch :234-248) */
+/* keyswitch_lwe_ciphertext_list_and_pack_in_glwe_ciphertext (FheContext::packing_keyswitch :240-254) */
 void or_s1_pack(const or_server_key *sk, const uint64_t *cts, int count, uint64_t *glwe);
-/* test_vector_from_ciphertexts (:375-466) */
+/* test_vector_from_ciphertexts (:392-492) */
 void or_s1_tv_from_cts(const or_server_key *sk, const uint64_t *ct0, const uint64_t *ct1, uint64_t *glwe);
-/* FheContext::bootstrap (:250-286): PBS with a test vector, then keyswitch back to the small key */
+/* FheContext::bootstrap / bootstrap_assign (:257-291): PBS with a test vector, then keyswitch back to the small key */
 void or_s1_bootstrap(const or_server_key *sk, const uint64_t *in, const uint64_t *tv, uint64_t *out);
-/* calculate_multivariate_function (:497-536) over bits [nbits][n+1] (MSB first) with the test vectors of
- * generate_multivariate_test_vector (:478-495) for f_table [2^nbits] (0/1 values) */
+/* calculate_multivariate_function (:538-547, apply_selectors_rec :549-576) over bits [nbits][n+1] (MSB first) with the test vectors of
+ * generate_multivariate_test_vector (:519-536) for f_table [2^nbits] (0/1 values) */
 void or_s1_multivariate(const or_server_key *sk, const uint64_t *bits, int nbits, const uint64_t *f_table,
                         uint64_t *out);
 void or_bootstrap_with_lut8(const or_server_key *sk, const uint64_t *bits, const uint64_t *lut, uint64_t *out);

@@ -121,6 +121,31 @@ def test_caller_stream_ordering(gpu_context, oracle_keys, client):
         assert np.array_equal(out[i], oracle_keys.keyswitch(cts[i])), i
 
 
+def test_caller_stream_key_schedule(gpu_context, client):
+    """The TAE_MEM_DEVICE key schedule downloads its key after the caller's stream: the key is produced
+    by a non-blocking copy on a torch side stream right before the call, and the device result must
+    equal the host-array call's (key schedule fhe_sbox_gal_mul_pbs.rs:134-164)."""
+    torch = pytest.importorskip("torch")
+    E = aes_128.ShortintWoppbs1BitSboxGalMulPbsAesEncrypt
+    key = client.encrypt_bits_raw(aes_128.blocks_to_bits([bytes(range(16))])[0], start_index=3_000_000)
+    ref = E.key_schedule_raw(gpu_context, key)
+    side = torch.cuda.Stream()
+    h = torch.from_numpy(key.view(np.int64)).pin_memory()
+    d_key = torch.zeros(h.shape, dtype=torch.int64, device="cuda")
+    d_out = torch.zeros((44 * 32, BIG), dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    try:
+        gpu_context.set_caller_stream(side)
+        with torch.cuda.stream(side):
+            d_key.copy_(h, non_blocking=True)
+            d_key.add_(0)
+        N.check(E._fn("key_schedule_raw")(gpu_context._h, C.c_void_p(d_key.data_ptr()),
+                                          C.c_void_p(d_out.data_ptr()), N.TAE_MEM_DEVICE))
+    finally:
+        gpu_context.set_caller_stream(None)
+    assert np.array_equal(d_out.cpu().numpy().view(np.uint64), ref)
+
+
 def test_context_shared_across_host_threads(gpu_context, client):
     """One context used from six host threads at once (the header's promise, and the reference's
     FheContext: Send + Sync): ctypes drops the GIL, the context's lock serialises the device work, and

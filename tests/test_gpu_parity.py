@@ -234,3 +234,18 @@ def test_aes_two_rounds_bit_exact_vs_oracle(gpu_context, oracle_keys, client, go
     assert aes_128.bits_to_blocks(client.decrypt_bits_raw(out))[0].hex() == g["block1"]["2"]
     ref = oracle_keys.aes_encrypt_block(rk, cts[0], 2, threads=16)
     assert np.array_equal(out[0], ref)
+
+
+def test_aes_ten_rounds_bit_exact_vs_oracle(gpu_context, oracle_keys, client, golden):
+    """test_full (aes_128/test_helper.rs:22-84) at configs[1]: one counter block (README key / iv,
+    counter 1) through all 10 rounds with a plain-expanded, encrypted round key.  Every ciphertext word
+    of the output equals the oracle's, and it decrypts to the README's counter-mode block."""
+    g = golden["readme_ctr"]
+    ek = b"".join(aes_128.key_schedule_plain(bytes.fromhex(g["key"])))
+    rk = client.encrypt_bits_raw([b for byte in ek for b in aes_128.u8_to_bits(byte)], start_index=50_000)
+    blk = bytes.fromhex(g["blocks"]["1"])
+    cts = client.encrypt_bits_raw(aes_128.blocks_to_bits([blk]), start_index=60_000).reshape(1, 128, BIG)
+    out = aes_128.ShortintWoppbs1BitSboxGalMulPbsAesEncrypt.encrypt_blocks_raw(gpu_context, rk, cts, rounds=10)
+    assert aes_128.bits_to_blocks(client.decrypt_bits_raw(out))[0].hex() == g["ciphertexts"]["1"]
+    ref = oracle_keys.aes_encrypt_block(rk, cts[0], 10, threads=16)
+    assert np.array_equal(out[0], ref)

@@ -67,7 +67,7 @@ def test_multivariate_parity_fn_3(okeys, byte):
 
 
 def test_test_vector_from_ciphertexts_layout(okeys):
-    """test_vector_from_ciphertexts (:375-466): ct0 fills [0, N/4) u [3N/4, N), ct1 [N/4, 3N/4) of the body
+    """test_vector_from_ciphertexts (:392-492): ct0 fills [0, N/4) u [3N/4, N), ct1 [N/4, 3N/4) of the body
     phase (the add-then-rotate loops of the reference restated step by step in the oracle)"""
     cts = okeys.s1_encrypt([1, 0], ES, 60)
     plain = okeys.glwe_decrypt(okeys.tv_from_cts(cts[0], cts[1]))

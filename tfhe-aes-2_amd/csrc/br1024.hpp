@@ -104,8 +104,10 @@ __global__ void __launch_bounds__(THREADS, 1)
     br_kernel(const uint64_t *__restrict__ lwe_in, int n, const uint64_t *__restrict__ lut, int n_out,
               const cplx *__restrict__ ggsw_base, int n_in, uint64_t *__restrict__ out, long B,
               uint64_t body_add, uint64_t out_add, const cplx *__restrict__ twist, const cplx *__restrict__ untwist,
-              const cplx *__restrict__ wtab) {
+              const cplx *__restrict__ wtab, uint64_t *__restrict__ clk) {
     static_assert(LEV % LP == 0, "levels per pass must divide the level count");
+    ClockStamp stamp;
+    stamp.start(clk);
     constexpr int LOGN = 10, CJ = C * K1, JOBS = CJ * LP;
     extern __shared__ __align__(16) unsigned char smem[];
     uint64_t *acc = reinterpret_cast<uint64_t *>(smem);           // [CJ][ACC_STRIDE]
@@ -434,6 +436,7 @@ __global__ void __launch_bounds__(THREADS, 1)
         }
         if (tid == 0) o[(K1 - 1) * N] = a[(K1 - 1) * ACC_STRIDE] + out_add;
     }
+    stamp.stop(clk);
 }
 
 #undef W0_AT
@@ -447,7 +450,7 @@ inline size_t lds_bytes(int C, int LP = 1) {
 
 // (levels, base_log) combinations of the N=1024 parameter sets: returns the kernel or nullptr
 typedef void (*kernel_t)(const uint64_t *, int, const uint64_t *, int, const cplx *, int, uint64_t *, long, uint64_t,
-                         uint64_t, const cplx *, const cplx *, const cplx *);
+                         uint64_t, const cplx *, const cplx *, const cplx *, uint64_t *);
 // LP levels per pass; LP = 2 only for the PBS with at least two passes (nullptr otherwise)
 template <int C, int LP = 1>
 inline kernel_t pick(bool pbs, int levels, int base_log) {

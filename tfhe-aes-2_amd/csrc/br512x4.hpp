@@ -153,8 +153,11 @@ template <int LEV, bool PBS, int BLOG>
 __global__ void __launch_bounds__(THREADS, 1)
     br_kernel(const uint64_t *__restrict__ lwe_in, int n, const uint64_t *__restrict__ lut, int n_out,
               const cplx *__restrict__ ggsw_base, int n_in, uint64_t *__restrict__ out, long B,
-              uint64_t body_add, uint64_t out_add, const cplx *__restrict__ twist, const cplx *__restrict__ wtab) {
+              uint64_t body_add, uint64_t out_add, const cplx *__restrict__ twist, const cplx *__restrict__ wtab,
+              uint64_t *__restrict__ clk) {
     constexpr int LOGN = 9;
+    ClockStamp stamp;
+    stamp.start(clk);
     extern __shared__ __align__(16) unsigned char smem[];
     uint64_t *acc = reinterpret_cast<uint64_t *>(smem);             // [JOBS][ACC_STRIDE]
     cplx *buf = reinterpret_cast<cplx *>(acc + JOBS * ACC_STRIDE);  // [JOBS][BUF_STRIDE]
@@ -418,6 +421,7 @@ __global__ void __launch_bounds__(THREADS, 1)
         }
         if (tid == 0) o[(K1 - 1) * N] = a[(K1 - 1) * ACC_STRIDE] + out_add;
     }
+    stamp.stop(clk);
 }
 
 inline size_t lds_bytes() {

@@ -757,7 +757,20 @@ int tae_set_caller_stream(tae_context *ctx, void *stream) {
 int tae_set_timing(const tae_context *ctx, int on) {
     return guarded([&] {
         require(ctx, "null");
-        ctx->ctx->engine().set_timing(on != 0);
+        require(on >= 0 && on <= 2, "timing mode is 0, 1 or 2");
+        ctx->ctx->engine().set_timing(on);
+    });
+}
+
+int tae_last_stage_times_v4(const tae_context *ctx, double *v12) {
+    return guarded([&] {
+        require(ctx && v12, "null");
+        const auto &t = ctx->ctx->engine().last_times();
+        const double v[12] = {t.keyswitch, t.pbs,    t.pfks,         t.ggsw_fft, t.vertical_packing,
+                              t.extract,   t.linear, (double)t.pbs_launches, t.pbs_main, t.pbs_main_cts,
+                              t.pbs_clock_launches ? t.pbs_clock_ghz_sum / t.pbs_clock_launches : 0.0,
+                              (double)t.pbs_clock_launches};
+        for (int i = 0; i < 12; i++) v12[i] = v[i];
     });
 }
 

@@ -34,6 +34,10 @@ struct StageTimes {
     // br512lat remainder) and the ciphertexts those launches processed
     float pbs_main = 0;
     double pbs_main_cts = 0;
+    // clock mode (set_timing(2)): median effective shader clock over the workgroups of each throughput
+    // blind-rotation launch (br512x4, or br1024 with two ciphertexts per workgroup), summed over launches
+    double pbs_clock_ghz_sum = 0;
+    int pbs_clock_launches = 0;
 };
 enum Stage { ST_KS = 0, ST_PBS, ST_PFKS, ST_FFT, ST_VP, ST_EXTRACT, ST_LINEAR, ST_PBS_MAIN };
 
@@ -98,19 +102,21 @@ class Engine {
                             uint64_t *d_out);
 
     // ---- shortint_1bit model (src/tfhe/shortint_1bit.rs; param set SHORTINT_1BIT) ----
-    // FheContext::bootstrap (:250-286): PBS with test vector d_tvs + (b % lut_mod) (k+1)N, then the keyswitch
+    // FheContext::bootstrap / bootstrap_assign (:257-291): PBS with test vector d_tvs + (b % lut_mod) (k+1)N, then the keyswitch
     // back to the small key: [B][n+1] -> [B][n+1]
     void s1_bootstrap(const uint64_t *d_in, const uint64_t *d_tvs, size_t lut_mod, uint64_t *d_out, size_t B);
     // keyswitch_lwe_ciphertext_into_glwe_ciphertext with the packing key, per ciphertext: [B][n+1] -> [B][(k+1)N]
     void s1_pks(const uint64_t *d_in, size_t B, uint64_t *d_out);
-    // test_vector_from_ciphertexts (:375-466) over P pairs of packing keyswitches [2P][(k+1)N] -> [P][(k+1)N]
+    // test_vector_from_ciphertexts (:392-492) over P pairs of packing keyswitches [2P][(k+1)N] -> [P][(k+1)N]
     void s1_tv_from_pks(const uint64_t *d_pks, size_t P, uint64_t *d_tv);
-    // FheContext::packing_keyswitch (:234-248): count ciphertexts into one GLWE, #j at X^j
+    // FheContext::packing_keyswitch (:240-254): count ciphertexts into one GLWE, #j at X^j
     void s1_pack(const uint64_t *d_in, int count, uint64_t *d_out);
-    // calculate_multivariate_function (:497-536) for n_fn functions of the same nbits bits, over G groups:
+    // calculate_multivariate_function (:538-547) / apply_selectors_rec (:549-576) for n_fn functions of the same nbits bits, over G groups:
     // bits [G][nbits][n+1] (MSB first), d_tvs [n_fn][2^(nbits-1)][(k+1)N] (generate_multivariate_test_vector)
     // -> [G][n_fn][n+1]; one batched bootstrap + packing step per selector level
     void s1_multivariate(const uint64_t *d_bits, size_t G, int nbits, const uint64_t *d_tvs, int n_fn, uint64_t *d_out);
+    void s1_multivariate_chunk(const uint64_t *d_bits, size_t G, int nbits, const uint64_t *d_tvs, int n_fn,
+                               uint64_t *d_out);
     // Shortint1BitSboxPbsAesEncrypt::encrypt_block_for_rounds over nb blocks: rk [44*32][n+1], blocks [nb][128][n+1]
     void s1_aes_encrypt_blocks(const uint64_t *d_rk, const uint64_t *d_blocks, size_t nb, int rounds, uint64_t *d_out);
     const uint64_t *s1_sbox_tvs() const { return d_s1_sbox_tv_; }  // [8][128][(k+1)N]
@@ -128,7 +134,12 @@ class Engine {
     // waits on an event recorded on this caller stream (no host sync, other streams not waited for)
     void set_caller_stream(hipStream_t s) { caller_stream_ = s; }
     const StageTimes &last_times() const { return times_; }
-    void set_timing(bool on) { timing_ = on; }
+    // 0 off, 1 HIP-event stage times, 2 stage times + in-kernel clock stamps of the blind rotations
+    // (a diagnostic mode: each stamped launch is read back synchronously)
+    void set_timing(int mode) {
+        timing_ = mode != 0;
+        clock_ = mode == 2;
+    }
 
     // scratch sizing: reserve buffers for a circuit_bootstrap of `bits` input bits
     void reserve(size_t bits, size_t outputs);
@@ -206,7 +217,7 @@ class Engine {
     void prepare_mfma_keys();
     // batched N=1024, k=2 blind rotation (br1024.hpp) for this set's (levels, base_log), or nullptr
     void (*br1024_pbs_)(const uint64_t *, int, const uint64_t *, int, const cplx *, int, uint64_t *, long, uint64_t,
-                        uint64_t, const cplx *, const cplx *, const cplx *) = nullptr;
+                        uint64_t, const cplx *, const cplx *, const cplx *, uint64_t *) = nullptr;
     decltype(br1024_pbs_) br1024_vp_ = nullptr;
     decltype(br1024_pbs_) br1024_pbs1_ = nullptr;  // one ciphertext per workgroup (small batches)
     int br1024_pbs1_lp_ = 1;                       // its levels per pass
@@ -217,7 +228,11 @@ class Engine {
     bool x4_512_ = false;     // N = 512, k = 4 (lvl_64): batched blind rotations br512x4 / br512lat
     long lat_max_ = 256;      // batch size up to which br512lat runs (TAE_BR_LAT_MAX)
     int num_cu_ = 256;
-    bool timing_ = false;
+    bool timing_ = false, clock_ = false;
+    uint64_t *d_clk_ = nullptr;
+    size_t cap_clk_ = 0;
+    uint64_t *clock_buffer(size_t wgs);                   // nullptr unless clock mode is on
+    void record_clock(const uint64_t *clk, size_t wgs);  // median GHz of one stamped launch
     StageTimes times_;
 };
 

@@ -338,6 +338,32 @@ __host__ __device__ __forceinline__ int32_t digit_next(uint32_t &st) {
     return (int32_t)res - (int32_t)(c << B);
 }
 
+// Effective-clock stamps of a blind-rotation launch (diagnostic launches only; every other launch passes
+// clk == nullptr and no stamp executes): the workgroup's shader cycles (s_memtime) and 100 MHz reference
+// ticks (s_memrealtime) from kernel entry to exit, written by thread 0 to clk[2 wg] / clk[2 wg + 1], a
+// buffer nothing else reads (MI355X_MICROARCH.md "DVFS give-back" item 6).  The stamps are wave-uniform
+// (SGPRs, no VGPR held across the kernel); lgkmcnt is drained after the first pair.
+struct ClockStamp {
+    uint64_t c0 = 0, r0 = 0;
+    __device__ __forceinline__ void start(const uint64_t *clk) {
+        if (clk) {
+            c0 = __builtin_amdgcn_s_memtime();
+            r0 = __builtin_amdgcn_s_memrealtime();
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+        }
+    }
+    __device__ __forceinline__ void stop(uint64_t *clk) {
+        if (clk) {
+            const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            if (threadIdx.x == 0) {
+                clk[2 * (size_t)blockIdx.x] = c1 - c0;
+                clk[2 * (size_t)blockIdx.x + 1] = r1 - r0;
+            }
+        }
+    }
+};
+
 // pbs_modulus_switch: round(x * 2N / 2^64) in [0, 2N]
 __device__ __forceinline__ int mod_switch(uint64_t x, int logN) {
     uint64_t o = x >> (64 - logN - 2);

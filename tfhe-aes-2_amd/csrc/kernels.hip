@@ -37,6 +37,7 @@ void hip_check(hipError_t e, const char *what) {
 namespace {
 
 constexpr int kThreads = 256;
+constexpr size_t kS1Rows = 16384;  // shortint_1bit selector trees: level-0 bootstraps per chunk
 
 // ---------------------------------------------------------------------------------------------
 // External product on an LDS-resident GLWE accumulator:
@@ -535,29 +536,57 @@ __global__ void aes8_mix_kernel(const uint64_t *__restrict__ sb, const uint64_t 
 }
 
 // ---- shortint_1bit model (src/tfhe/shortint_1bit.rs) ----
-// test_vector_from_ciphertexts (:375-466) for pair p: with P0 / P1 the packing keyswitches of the two
+// test_vector_from_ciphertexts (shortint_1bit.rs:392-492) for pair p: with P0 / P1 the packing keyswitches of the two
 // ciphertexts, tv = sum_{i in [0, N/4) u [3N/4, N)} X^i P0 + sum_{i in [N/4, 3N/4)} X^i P1 (negacyclic,
 // wrapping u64: the reference's add-then-rotate loops in closed form).  One workgroup per (pair, polynomial).
+// The term of shift i is E[t + N - i] of the negacyclic extension E = [-P, P] (length 2N), so each run of
+// shifts with one source is a window of E: tv[t] = sum over the three runs of Pre[t + N - i0 + 1] -
+// Pre[t + N - i1 + 1], Pre the exclusive prefix sums of E (mod 2^64, hence exact): O(N) per polynomial.
 template <int N>
 __global__ void __launch_bounds__(kThreads) s1_tv_kernel(const uint64_t *__restrict__ pks, uint64_t *__restrict__ tv, int k) {
-    __shared__ uint64_t a[N], b[N];
+    constexpr int PER = 2 * N / kThreads;
+    static_assert(PER * kThreads == 2 * N, "s1_tv_kernel shape");
+    __shared__ uint64_t pa[2 * N + 1], pb[2 * N + 1], part[2][kThreads];
     const size_t pair = blockIdx.x / (k + 1);
     const int c = blockIdx.x - (int)pair * (k + 1);
     const size_t glwe = (size_t)(k + 1) * N;
     const uint64_t *p0 = pks + 2 * pair * glwe + (size_t)c * N, *p1 = p0 + glwe;
-    for (int t = threadIdx.x; t < N; t += blockDim.x) {
-        a[t] = p0[t];
-        b[t] = p1[t];
+    const int tid = threadIdx.x, y0 = tid * PER;
+    uint64_t xa[PER], xb[PER], sa = 0, sb = 0;
+#pragma unroll
+    for (int j = 0; j < PER; j++) {
+        const int y = y0 + j;
+        xa[j] = y < N ? 0 - p0[y] : p0[y - N];
+        xb[j] = y < N ? 0 - p1[y] : p1[y - N];
+        sa += xa[j];
+        sb += xb[j];
+    }
+    part[0][tid] = sa;
+    part[1][tid] = sb;
+    __syncthreads();
+    for (int off = 1; off < kThreads; off <<= 1) {  // inclusive scan of the per-thread sums
+        const uint64_t ua = tid >= off ? part[0][tid - off] : 0, ub = tid >= off ? part[1][tid - off] : 0;
+        __syncthreads();
+        part[0][tid] += ua;
+        part[1][tid] += ub;
+        __syncthreads();
+    }
+    uint64_t ea = tid ? part[0][tid - 1] : 0, eb = tid ? part[1][tid - 1] : 0;
+#pragma unroll
+    for (int j = 0; j < PER; j++) {
+        pa[y0 + j] = ea;
+        pb[y0 + j] = eb;
+        ea += xa[j];
+        eb += xb[j];
+    }
+    if (tid == kThreads - 1) {
+        pa[2 * N] = ea;
+        pb[2 * N] = eb;
     }
     __syncthreads();
-    for (int t = threadIdx.x; t < N; t += blockDim.x) {
-        uint64_t acc = 0;
-        for (int i = 0; i < N; i++) {
-            const int src = t - i;
-            const bool wrap = src < 0;
-            const uint64_t v = (i < N / 4 || i >= 3 * N / 4) ? a[wrap ? src + N : src] : b[wrap ? src + N : src];
-            acc += wrap ? (0 - v) : v;
-        }
+    for (int t = tid; t < N; t += kThreads) {
+        const int z = t + N + 1;  // window of the run [i0, i1): Pre[z - i0] - Pre[z - i1]
+        const uint64_t acc = (pa[z] - pa[z - N / 4]) + (pb[z - N / 4] - pb[z - 3 * N / 4]) + (pa[z - 3 * N / 4] - pa[z - N]);
         tv[pair * glwe + (size_t)c * N + t] = acc;
     }
 }
@@ -616,6 +645,8 @@ template <class T>
 T *Engine::grow(T *&ptr, size_t &cap, size_t count) {
     if (count > cap) {
         if (ptr) HIPC(hipFree(ptr));
+        ptr = nullptr;  // a failing alloc below must not leave a freed pointer for ~Engine
+        cap = 0;
         ptr = static_cast<T *>(alloc(count * sizeof(T)));
         cap = count;
     }
@@ -659,7 +690,7 @@ void Engine::init_common() {
     if (p_.model == 2) {
         // shortint_1bit ByteT (fhe_impls/shortint_1bit.rs:17-50): bootstrap_assign's identity test vector
         // and sbox_substitute's 8 multivariate test vectors (one per output bit, MSB first), each the
-        // 128 cleartext test vectors of generate_multivariate_test_vector (shortint_1bit.rs:478-495)
+        // 128 cleartext test vectors of generate_multivariate_test_vector (shortint_1bit.rs:519-536)
         const size_t glwe = p_.glwe_len(), V = 128;
         std::vector<uint64_t> tvs(8 * V * glwe), id(glwe);
         for (int f = 0; f < 8; f++)
@@ -887,7 +918,7 @@ Engine::~Engine() {
                     (void *)d_ggsw_f_, (void *)d_state_, (void *)d_muls_, (void *)d_pf_bt_, (void *)d_ks_bt_, (void *)d_pf_corr_, (void *)d_pf_bt_kl_,
                     (void *)d_digits_, (void *)d_wlut_sbox_, (void *)d_wlut_id_, (void *)d_lut_x_, (void *)d_xbuf_,
                     (void *)d_xsh_, (void *)d_xks_, (void *)d_xpbs_, (void *)d_ints_, (void *)d_s1_sbox_tv_,
-                    (void *)d_s1_id_tv_, (void *)d_s1_in_, (void *)d_s1_out_, (void *)d_s1_pks_, (void *)d_s1_tv_, (void *)d_pf_flags_})
+                    (void *)d_s1_id_tv_, (void *)d_s1_in_, (void *)d_s1_out_, (void *)d_s1_pks_, (void *)d_s1_tv_, (void *)d_pf_flags_, (void *)d_clk_})
         if (q) hipFree(q);
     for (auto &e : ev_pool_) hipEventDestroy(e);
     if (caller_ev_) hipEventDestroy(caller_ev_);
@@ -953,12 +984,14 @@ void Engine::bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint
         long bx = (long)B;
         const long per_round = 3L * num_cu_, rest = (long)B % per_round;
         if ((long)B > per_round && rest > 0 && rest <= std::min<long>(lat_max_, num_cu_)) bx -= rest;
+        const unsigned wgs = (unsigned)((bx + 2) / 3);
+        uint64_t *clk = clock_buffer(wgs);
         timed(ST_PBS_MAIN, [&] {
-            br512x4::br_kernel<3, true, 12><<<(unsigned)((bx + 2) / 3), br512x4::THREADS, br512x4::lds_bytes(),
-                                               stream_>>>(d_small, p_.n, d_lut_glwe, 0, d_bsk_f_, 0, d_big, bx,
-                                                          body_add, out_add, d_twist_, d_w_);
+            br512x4::br_kernel<3, true, 12><<<wgs, br512x4::THREADS, br512x4::lds_bytes(), stream_>>>(
+                d_small, p_.n, d_lut_glwe, 0, d_bsk_f_, 0, d_big, bx, body_add, out_add, d_twist_, d_w_, clk);
             HIPC(hipGetLastError());
         });
+        record_clock(clk, wgs);
         if (timing_) times_.pbs_main_cts += (double)bx;
         if (bx < (long)B) {
             br512lat::br_kernel<3, 12><<<(unsigned)(B - bx), br512lat::THREADS, br512lat::lds_bytes(3), stream_>>>(
@@ -978,10 +1011,13 @@ void Engine::bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint
         // two ciphertexts per workgroup share its GGSW loads, but below one per CU they leave CUs idle
         const int C = (long)B <= (long)num_cu_ ? 1 : 2;
         const size_t wgs = (B + C - 1) / C;
+        uint64_t *clk = C == 2 ? clock_buffer(wgs) : nullptr;  // the throughput instantiation only
         (C == 1 ? br1024_pbs1_ : br1024_pbs_)<<<(unsigned)wgs, br1024::THREADS, br1024::lds_bytes(C, C == 1 ? br1024_pbs1_lp_ : 1),
                                                               stream_>>>(
-            d_small, p_.n, d_lut_glwe, 0, d_bsk_f_, 0, d_big, (long)B, body_add, out_add, d_twist_, d_untwist_, d_w_);
+            d_small, p_.n, d_lut_glwe, 0, d_bsk_f_, 0, d_big, (long)B, body_add, out_add, d_twist_, d_untwist_, d_w_,
+            clk);
         HIPC(hipGetLastError());
+        record_clock(clk, wgs);
         return;
     }
     for (size_t off = 0; off < B; off += 65535) {
@@ -1018,11 +1054,7 @@ void Engine::pfks_into_ggsw(const uint64_t *d_big, uint64_t *d_ggsw, size_t B, i
         const int fw = (int)(((size_t)(K + 1) * p_.pfks_l + 31) / 32);  // flag words per ciphertext
         if (clamp) {
             const size_t need = B * (size_t)fw;
-            if (need > cap_pf_flags_) {
-                if (d_pf_flags_) HIPC(hipFree(d_pf_flags_));
-                HIPC(hipMalloc(&d_pf_flags_, need * 4));
-                cap_pf_flags_ = need;
-            }
+            grow(d_pf_flags_, cap_pf_flags_, need);
             HIPC(hipMemsetAsync(d_pf_flags_, 0, need * 4, stream_));
         }
         ksgemm::prep_digits_kl<<<(unsigned)((thr + 255) / 256), 256, 0, stream_>>>(
@@ -1134,14 +1166,14 @@ void Engine::vertical_packing(const cplx *d_ggsw_f, size_t G, int n_in, const ui
     if (x4_512_) {
         const size_t wgs = G * (size_t)((n_out + kBrC - 1) / kBrC);
         br512x4::br_kernel<1, false, 13><<<(unsigned)wgs, br512x4::THREADS, br512x4::lds_bytes(), stream_>>>(
-            nullptr, 0, d_lut, n_out, d_ggsw_f, n_in, d_out, (long)G, 0, 0, d_twist_, d_w_);
+            nullptr, 0, d_lut, n_out, d_ggsw_f, n_in, d_out, (long)G, 0, 0, d_twist_, d_w_, nullptr);
         HIPC(hipGetLastError());
         return;
     }
     if (br1024_vp_) {
         const size_t wgs = G * (size_t)((n_out + 1) / 2);
         br1024_vp_<<<(unsigned)wgs, br1024::THREADS, br1024::lds_bytes(2), stream_>>>(
-            nullptr, 0, d_lut, n_out, d_ggsw_f, n_in, d_out, (long)G, 0, 0, d_twist_, d_untwist_, d_w_);
+            nullptr, 0, d_lut, n_out, d_ggsw_f, n_in, d_out, (long)G, 0, 0, d_twist_, d_untwist_, d_w_, nullptr);
         HIPC(hipGetLastError());
         return;
     }
@@ -1181,6 +1213,28 @@ void Engine::timed(int stage, F fn) {
     fn();
     HIPC(hipEventRecord(sp.b, stream_));
     spans_.push_back(sp);
+}
+
+uint64_t *Engine::clock_buffer(size_t wgs) {
+    if (!clock_) return nullptr;
+    grow(d_clk_, cap_clk_, 2 * wgs);
+    HIPC(hipMemsetAsync(d_clk_, 0, 2 * wgs * 8, stream_));
+    return d_clk_;
+}
+
+void Engine::record_clock(const uint64_t *clk, size_t wgs) {
+    if (!clk) return;
+    std::vector<uint64_t> h(2 * wgs);
+    HIPC(hipMemcpyAsync(h.data(), clk, h.size() * 8, hipMemcpyDeviceToHost, stream_));
+    HIPC(hipStreamSynchronize(stream_));
+    std::vector<double> ghz;
+    ghz.reserve(wgs);
+    for (size_t w = 0; w < wgs; w++)
+        if (h[2 * w + 1] > 0) ghz.push_back((double)h[2 * w] / (double)h[2 * w + 1] * 0.1);  // 100 MHz reference
+    if (ghz.empty()) return;
+    std::nth_element(ghz.begin(), ghz.begin() + ghz.size() / 2, ghz.end());
+    times_.pbs_clock_ghz_sum += ghz[ghz.size() / 2];
+    times_.pbs_clock_launches += 1;
 }
 
 void Engine::collect_times() {
@@ -1375,6 +1429,19 @@ void Engine::s1_multivariate(const uint64_t *d_bits, size_t G, int nbits, const 
     require_s1();
     if (!G) return;
     if (nbits < 1 || nbits > 8) throw std::runtime_error("multivariate functions take 1..8 bits");
+    // groups are independent: run them in chunks whose level-0 batch stays near kS1Rows bootstraps, so the
+    // scratch (~60 KB per row: inputs, outputs, big LWEs, packing keyswitches, test vectors) is bounded
+    // (~1 GB) whatever the batch, and a chunk still fills the chip
+    const size_t rows_per_group = (size_t)n_fn << (nbits - 1);
+    const size_t gc = std::max<size_t>(1, kS1Rows / rows_per_group);
+    const size_t L = p_.small_len();
+    for (size_t g0 = 0; g0 < G; g0 += gc)
+        s1_multivariate_chunk(d_bits + g0 * nbits * L, std::min(gc, G - g0), nbits, d_tvs, n_fn,
+                              d_out + g0 * n_fn * L);
+}
+
+void Engine::s1_multivariate_chunk(const uint64_t *d_bits, size_t G, int nbits, const uint64_t *d_tvs, int n_fn,
+                                   uint64_t *d_out) {
     const int L = p_.n + 1;
     const size_t glwe = p_.glwe_len();
     size_t V = (size_t)1 << (nbits - 1), B = G * n_fn * V;
@@ -1385,7 +1452,7 @@ void Engine::s1_multivariate(const uint64_t *d_bits, size_t G, int nbits, const 
     const uint64_t *tvs = d_tvs;
     size_t lut_mod = (size_t)n_fn * V;  // level 0: the cleartext test vectors, shared by every group
     for (int sel = nbits - 1;; sel--) {
-        // apply_selectors_rec (shortint_1bit.rs:510-536): bootstrap every test vector of (group, fn) with
+        // apply_selectors_rec (shortint_1bit.rs:549-576): bootstrap every test vector of (group, fn) with
         // the group's selector bit sel, then pack the results pairwise into the next level's vectors
         s1_gather_kernel<<<grid_for(B * L), kThreads, 0, stream_>>>(d_bits, d_s1_in_, B, (size_t)n_fn * V, nbits, sel, L);
         HIPC(hipGetLastError());

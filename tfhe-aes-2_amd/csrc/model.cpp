@@ -698,7 +698,11 @@ void Context::aes_key_schedule_raw(const uint64_t *key, uint64_t *expanded, bool
     if (device_mem) {
         std::lock_guard<std::mutex> g(mu_);  // the engine (and its device) is shared: same lock as every entry
         engine_->order_after_caller();
-        hip_check(hipMemcpy(hk.data(), key, hk.size() * 8, hipMemcpyDeviceToHost), "download key");
+        // on the engine stream, which waits for the caller's stream (a plain hipMemcpy runs on the null
+        // stream, which does not wait for a non-blocking caller stream)
+        hip_check(hipMemcpyAsync(hk.data(), key, hk.size() * 8, hipMemcpyDeviceToHost, engine_->stream()),
+                  "download key");
+        engine_->synchronize();
     } else {
         std::memcpy(hk.data(), key, hk.size() * 8);
     }
@@ -711,9 +715,12 @@ void Context::aes_key_schedule_raw(const uint64_t *key, uint64_t *expanded, bool
     const std::vector<BitCt> ek = aes_key_schedule(kp, driver);
     std::vector<uint64_t> he(44 * 32 * L);
     for (size_t i = 0; i < ek.size(); i++) std::memcpy(&he[i * L], ek[i].ct.data(), L * 8);
-    if (device_mem)
-        hip_check(hipMemcpy(expanded, he.data(), he.size() * 8, hipMemcpyHostToDevice), "upload expanded key");
-    else
+    if (device_mem) {
+        std::lock_guard<std::mutex> g(mu_);
+        hip_check(hipMemcpyAsync(expanded, he.data(), he.size() * 8, hipMemcpyHostToDevice, engine_->stream()),
+                  "upload expanded key");
+        engine_->synchronize();
+    } else
         std::memcpy(expanded, he.data(), he.size() * 8);
 }
 
@@ -788,7 +795,7 @@ void Context::s1_multivariate_raw(const uint64_t *bits, size_t G, int nbits, con
     if (nbits < 1 || nbits > 8) throw ModelError{TAE_E_ARG, "multivariate functions take 1..=8 bits (shortint_1bit.rs:526)"};
     if (n_fn < 1) throw ModelError{TAE_E_ARG, "at least one function"};
     const size_t L = bit_len(), GL = params().glwe_len(), V = (size_t)1 << (nbits - 1);
-    // generate_multivariate_test_vector (:478-495): test vector v of function f selects f(2v + bit)
+    // generate_multivariate_test_vector (:519-536): test vector v of function f selects f(2v + bit)
     std::vector<uint64_t> tvs((size_t)n_fn * V * GL);
     for (int f = 0; f < n_fn; f++)
         for (size_t v = 0; v < V; v++) {

@@ -33,7 +33,7 @@ EXPORTED = [
     "tae_synchronize", "tae_set_caller_stream", "tae_set_timing", "tae_last_stage_times", "tae_bit_len", "tae_encrypt_ints_raw",
     "tae_decrypt_ints_raw", "tae_bootstrap_from_bits_raw", "tae_extract_bits_raw", "tae_aes_key_schedule_raw",
     "tae_last_stage_times_v2", "tae_keys_save", "tae_keys_file_info", "tae_keys_load",
-    "tae_last_stage_times_v3", "tae_generate_multivariate_luts", "tae_xor_batch",
+    "tae_last_stage_times_v3", "tae_last_stage_times_v4", "tae_generate_multivariate_luts", "tae_xor_batch",
     "tae_aes_sbox_pbs_encrypt_blocks", "tae_aes_sbox_pbs_key_schedule", "tae_aes_sbox_pbs_encrypt_blocks_raw",
     "tae_aes_sbox_pbs_key_schedule_raw", "tae_aes_noise_schedule_check",
     "tae_s1_test_vector_from_fn", "tae_s1_bootstrap", "tae_s1_packing_keyswitch",
@@ -135,6 +135,7 @@ def lib() -> C.CDLL:
         "tae_aes_key_schedule_raw": ([vp, vp, vp, C.c_int], C.c_int),
         "tae_last_stage_times_v2": ([vp, C.POINTER(C.c_float)], C.c_int),
         "tae_last_stage_times_v3": ([vp, C.POINTER(C.c_double)], C.c_int),
+        "tae_last_stage_times_v4": ([vp, C.POINTER(C.c_double)], C.c_int),
         "tae_generate_multivariate_luts": ([C.c_int, C.c_int, C.c_int, vp, vp, sz], C.c_int),
         "tae_xor_batch": ([vp, vp, vp, sz, vp, vp, vp, C.c_int], C.c_int),
         "tae_keys_save": ([C.c_char_p, C.c_int, vp, vp, vp, vp], C.c_int),

@@ -44,7 +44,7 @@ def _glwe_len(ctx: FheContext) -> int:
 
 
 class TestVector:
-    """TestVector (:289-291): the GLWE accumulator a bootstrap rotates, [(k+1)N] u64."""
+    """TestVector (:293-294): the GLWE accumulator a bootstrap rotates, [(k+1)N] u64."""
     __test__ = False  # not a pytest class
 
     def __init__(self, data: np.ndarray):
@@ -58,14 +58,14 @@ def _bits_array(bits) -> np.ndarray:
 
 
 def test_vector_from_cleartext_fn(ctx: FheContext, f: Callable[[Cleartext], Cleartext]) -> TestVector:
-    """FheContext::test_vector_from_cleartext_fn (:301-314)."""
+    """FheContext::test_vector_from_cleartext_fn (:208-221, free fn :365-390)."""
     out = np.zeros(_glwe_len(ctx), dtype=np.uint64)
     check(lib().tae_s1_test_vector_from_fn(PARAMS, _clear(f(Cleartext(0))), _clear(f(Cleartext(1))), _vp(out)))
     return TestVector(out)
 
 
 def test_vectors_from_ciphertexts(ctx: FheContext, bits0, bits1) -> np.ndarray:
-    """FheContext::test_vector_from_ciphertexts (:316-332) for many pairs at once: [count][(k+1)N]."""
+    """FheContext::test_vector_from_ciphertexts (:225-237, free fn :392-492) for many pairs at once: [count][(k+1)N]."""
     a, b = _bits_array(bits0), _bits_array(bits1)
     if a.shape != b.shape:
         raise ValueError("the two ciphertext lists must have the same shape")
@@ -79,7 +79,7 @@ def test_vector_from_ciphertexts(ctx: FheContext, bit0, bit1) -> TestVector:
 
 
 def packing_keyswitch(ctx: FheContext, cts) -> np.ndarray:
-    """FheContext::packing_keyswitch (:234-248): GLWE [(k+1)N] with ciphertext j at coefficient j."""
+    """FheContext::packing_keyswitch (:240-254): GLWE [(k+1)N] with ciphertext j at coefficient j."""
     a = _bits_array(cts)
     out = np.zeros(_glwe_len(ctx), dtype=np.uint64)
     check(lib().tae_s1_packing_keyswitch(ctx._h, _vp(a), a.shape[0], _vp(out), N.TAE_MEM_HOST))
@@ -87,7 +87,7 @@ def packing_keyswitch(ctx: FheContext, cts) -> np.ndarray:
 
 
 def bootstrap_raw(ctx: FheContext, cts, tvs) -> np.ndarray:
-    """FheContext::bootstrap (:250-255) over many bits: cts [B][n+1], tvs one TestVector / [n_tv][(k+1)N]
+    """FheContext::bootstrap (:257-262, bootstrap_assign :264-291) over many bits: cts [B][n+1], tvs one TestVector / [n_tv][(k+1)N]
     (bit b takes tvs[b % n_tv])."""
     a = _bits_array(cts)
     t = _u64(tvs.data if isinstance(tvs, TestVector) else tvs).reshape(-1, _glwe_len(ctx))
@@ -97,12 +97,12 @@ def bootstrap_raw(ctx: FheContext, cts, tvs) -> np.ndarray:
 
 
 def bootstrap(ctx: FheContext, bit: BitCt, tv: TestVector) -> BitCt:
-    """FheContext::bootstrap (:250-255): a new bit, noise reset, test vector applied."""
+    """FheContext::bootstrap (:257-262): a new bit, noise reset, test vector applied."""
     return ctx.bit_from_data(bootstrap_raw(ctx, [bit], tv)[0], 0)
 
 
 class MultivariateTestVector:
-    """MultivariateTestVector (:470-476): the function table and its 2^(bits-1) cleartext test vectors
+    """MultivariateTestVector (:512-517): the function table and its 2^(bits-1) cleartext test vectors
     (generated on the device side from the table)."""
     __test__ = False
 
@@ -112,14 +112,14 @@ class MultivariateTestVector:
 
 
 def generate_multivariate_test_vector(ctx: FheContext, bits: int, f: Callable[[int], Cleartext]) -> MultivariateTestVector:
-    """generate_multivariate_test_vector (:478-495); f takes the u8 index of the bits (MSB first)."""
+    """generate_multivariate_test_vector (:519-536); f takes the u8 index of the bits (MSB first)."""
     if not 0 < bits <= 8:
         raise ValueError("0 < bits <= 8 (shortint_1bit.rs:526)")
     return MultivariateTestVector(bits, [_clear(f(v)) for v in range(1 << bits)])
 
 
 def calculate_multivariate_function_raw(ctx: FheContext, bits: np.ndarray, mv: Sequence[MultivariateTestVector]) -> np.ndarray:
-    """calculate_multivariate_function (:497-505) of several functions of the same bits, over many groups:
+    """calculate_multivariate_function (:538-547, apply_selectors_rec :549-576) of several functions of the same bits, over many groups:
     bits [G][nbits][n+1] -> [G][len(mv)][n+1] (one batched bootstrap + packing step per selector level)."""
     nb = mv[0].bits
     if any(m.bits != nb for m in mv):
@@ -132,7 +132,7 @@ def calculate_multivariate_function_raw(ctx: FheContext, bits: np.ndarray, mv: S
 
 
 def calculate_multivariate_function(ctx: FheContext, bit_cts, mv_test_vector: MultivariateTestVector) -> BitCt:
-    """calculate_multivariate_function (:497-505): bit_cts MSB first, len == mv_test_vector.bits."""
+    """calculate_multivariate_function (:538-547): bit_cts MSB first, len == mv_test_vector.bits."""
     a = _bits_array(bit_cts)
     if a.shape[0] != mv_test_vector.bits:
         raise ValueError("number of bits does not match the test vector (:502)")

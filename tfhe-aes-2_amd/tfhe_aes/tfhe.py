@@ -201,15 +201,19 @@ class FheContext:
         handle = getattr(stream, "cuda_stream", stream)
         check(lib().tae_set_caller_stream(self._h, C.c_void_p(handle) if handle else None))
 
-    def set_timing(self, on: bool):
-        check(lib().tae_set_timing(self._h, 1 if on else 0))
+    def set_timing(self, on, clock: bool = False):
+        """Per-stage HIP-event times of each batched call; clock=True also stamps the throughput blind-
+        rotation launches in-kernel (effective shader clock, read back synchronously: diagnostic only)."""
+        check(lib().tae_set_timing(self._h, (2 if clock else 1) if on else 0))
 
     def last_stage_times(self) -> dict:
-        arr = (C.c_double * 10)()
-        check(lib().tae_last_stage_times_v3(self._h, arr))
+        arr = (C.c_double * 12)()
+        check(lib().tae_last_stage_times_v4(self._h, arr))
         d = dict(zip(("keyswitch", "pbs", "pfks", "ggsw_fft", "vertical_packing", "extract_bits", "linear"), list(arr)))
         d["pbs_launches"] = int(arr[7])
         d["pbs_main"], d["pbs_main_cts"] = arr[8], arr[9]
+        if arr[11] > 0:
+            d["pbs_clock_ghz"], d["pbs_clock_launches"] = arr[10], int(arr[11])
         return d
 
     def xor_batch(self, lhs: np.ndarray, rhs: np.ndarray, lhs_noise_sq=None, rhs_noise_sq=None):
