@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU-box: PMC passes over the PFKS-only timing script (scripts/debug/time_pfks.py), one pass per
+# GPU-box: PMC passes over the PFKS-only timing script (scripts/ab/time_stage.py pfks1), one pass per
 # counter group; raw CSVs under gpurun_out/pmc_pfks_*/, per-kernel averages in gpurun_out/pmc_pfks.txt.
 set -o pipefail
 ROOT="$(cd "$(dirname "$0")/../.." && pwd)"
@@ -11,7 +11,7 @@ for grp in "SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_A
            "TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum SQ_WAVES SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU" \
            "TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum TCC_EA0_RDREQ_sum GRBM_GUI_ACTIVE"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d "$OUT/pmc_pfks_$i" -o run -- python3 "$ROOT/scripts/debug/time_pfks.py" > "$OUT/pmc_pfks_$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/pmc_pfks_$i.log"; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d "$OUT/pmc_pfks_$i" -o run -- python3 "$ROOT/scripts/ab/time_stage.py" pfks1 > "$OUT/pmc_pfks_$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/pmc_pfks_$i.log"; exit 1; }
 done
 python3 - "$OUT" > "$OUT/pmc_pfks.txt" <<'PY'
 import csv, glob, sys, collections

@@ -71,6 +71,16 @@ __device__ __forceinline__ cplx csel(bool c, cplx a, cplx b) { return {c ? a.re 
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+// msk ? b : a for a wave-uniform all-ones / all-zeros msk, as a VOP3 select on an SGPR pair (the compiler's
+// own form reads the condition from VCC)
+__device__ __forceinline__ uint32_t sel_sgpr(uint32_t a, uint32_t b, bool c) {
+    const uint64_t msk = ((uint64_t)__builtin_amdgcn_readfirstlane(c ? ~0u : 0u) << 32) |
+                         __builtin_amdgcn_readfirstlane(c ? ~0u : 0u);
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(msk));
+    return r;
+}
+
 // dft<8, 512, INV> of fft_device.hpp with the W8 factors from the table (w[64] = W8^1, w[192] = W8^3)
 template <bool INV>
 __device__ __forceinline__ void dft8(cplx *v, cplx w1, cplx w3) {
@@ -278,11 +288,16 @@ __global__ void __launch_bounds__(THREADS, 1)
                     if constexpr (BYTES) {
                         const int wsel = (lev - 1) >> 1, sh = ((lev - 1) & 1) * 16;
                         uint32_t dw = dig[0][m];
+#ifdef TAE_B1K_SGPRSEL
+#pragma unroll
+                        for (int w = 1; w < DW; w++) dw = sel_sgpr(dw, dig[w][m], wsel == w);
+#else
 #pragma unroll
                         for (int w = 1; w < DW; w++) {  // mask select (a ternary became a scratch index)
                             const uint32_t msk = 0u - (uint32_t)(wsel == w);
                             dw = (dw & ~msk) | (dig[w][m] & msk);
                         }
+#endif
                         a0 = (double)(int32_t)__builtin_amdgcn_sbfe(dw, sh, 8);
                         a1 = (double)(int32_t)__builtin_amdgcn_sbfe(dw, sh + 8, 8);
                     } else {

@@ -221,6 +221,7 @@ class Engine {
     decltype(br1024_pbs_) br1024_vp_ = nullptr;
     decltype(br1024_pbs_) br1024_pbs1_ = nullptr;  // one ciphertext per workgroup (small batches)
     int br1024_pbs1_lp_ = 1;                       // its levels per pass
+    bool br1024s_ = false;                         // br1024s.hpp for two ciphertexts per workgroup
     // latency blind rotation, one ciphertext per 1024-thread workgroup (br1024lat.hpp), or nullptr
     void (*br1024lat_)(const uint64_t *, int, const uint64_t *, const cplx *, uint64_t *, long, uint64_t, uint64_t,
                        const cplx *, const cplx *, const cplx *) = nullptr;

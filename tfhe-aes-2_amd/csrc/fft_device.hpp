@@ -179,6 +179,23 @@ __host__ __device__ __forceinline__ uint64_t torus_add_fast(double x, uint64_t a
     return acc + (mag ^ sg) + carry;
 }
 
+// torus_add_fast of x * 2^-SH (exact power-of-two scaling folded into the exponent): the untwist
+// conj(twist) / M of the inverse FFT is conj(twist) times an exact 2^-log2(M), so a kernel holding the twist
+// factors can multiply by conj(twist) and let the conversion apply the 2^-log2(M) (same result bit for bit
+// as the product with the untwist table, outside the subnormal range, which no value here reaches).
+template <int SH>
+__host__ __device__ __forceinline__ uint64_t torus_add_fast_sh(double x, uint64_t acc, bool &ok) {
+    const uint64_t b = f64_bits(x);
+    const uint32_t hi = (uint32_t)(b >> 32);
+    const uint32_t s = ((hi >> 20) & 0x7ff) - (1011u + SH);
+    ok = s <= 63u;
+    const uint64_t m = (b & 0xFFFFFFFFFFFFFull) | (1ull << 52);
+    const uint64_t mag = m << (s & 63);
+    const uint64_t sg = (uint64_t)(int64_t)((int32_t)hi >> 31);
+    const uint64_t carry = (uint64_t)((hi >> 31) & (uint32_t)(mag != 0x8000000000000000ull));
+    return acc + (mag ^ sg) + carry;
+}
+
 // tfhe-rs SignedDecomposer (closest_representable + balanced digits, the carry rule of
 // decompose_one_level) for LEV levels of B bits with B * (LEV - 1) < 32: d[l] = the 16-bit two's
 // complement pattern of the digit of level l + 1 (1 = most significant), upper half zero.

@@ -23,6 +23,7 @@
 #include "br512lat.hpp"
 #include "br1024.hpp"
 #include "br1024lat.hpp"
+#include "br1024s.hpp"
 #include "ksgemm.hpp"
 #include "engine.hpp"
 #include "fft_device.hpp"
@@ -765,6 +766,14 @@ void Engine::init_common() {
         // one ciphertext per 1024-thread workgroup, three levels per pass (the 8-bit model's PBS;
         // TAE_B1K_LAT=0: br1024's one-ciphertext kernel instead)
         const char *blat = getenv("TAE_B1K_LAT");
+        // two ciphertexts per workgroup with the FFT jobs streamed across the levels (the 8-bit model's PBS;
+        // TAE_B1K_STREAM=0: br1024's level-by-level kernel instead)
+        const char *bstr = getenv("TAE_B1K_STREAM");
+        if (p_.pbs_l == br1024s::LEV && p_.pbs_b == br1024s::BLOG && !(bstr && bstr[0] == '0')) {
+            br1024s_ = true;
+            HIPC(hipFuncSetAttribute((const void *)br1024s::br_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)br1024s::lds_bytes()));
+        }
         if (p_.pbs_l == 6 && p_.pbs_b == 7 && !(blat && blat[0] == '0')) {
             br1024lat_ = br1024lat::br_kernel<6, 7, 3>;
             br1024lat_lds_ = br1024lat::lds_bytes<6, 7, 3>();
@@ -1012,6 +1021,13 @@ void Engine::bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint
         const int C = (long)B <= (long)num_cu_ ? 1 : 2;
         const size_t wgs = (B + C - 1) / C;
         uint64_t *clk = C == 2 ? clock_buffer(wgs) : nullptr;  // the throughput instantiation only
+        if (C == 2 && br1024s_) {
+            br1024s::br_kernel<<<(unsigned)wgs, br1024s::THREADS, br1024s::lds_bytes(), stream_>>>(
+                d_small, p_.n, d_lut_glwe, d_bsk_f_, d_big, (long)B, body_add, out_add, d_twist_, d_w_, clk);
+            HIPC(hipGetLastError());
+            record_clock(clk, wgs);
+            return;
+        }
         (C == 1 ? br1024_pbs1_ : br1024_pbs_)<<<(unsigned)wgs, br1024::THREADS, br1024::lds_bytes(C, C == 1 ? br1024_pbs1_lp_ : 1),
                                                               stream_>>>(
             d_small, p_.n, d_lut_glwe, 0, d_bsk_f_, 0, d_big, (long)B, body_add, out_add, d_twist_, d_untwist_, d_w_,
