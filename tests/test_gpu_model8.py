@@ -64,8 +64,8 @@ def test_pbs8_kernel_variants_bit_exact(product_raw8, oracle_keys8, client8, lat
     """The N=1024 blind-rotation variants the engine picks: for batches up to one ciphertext per CU
     the 1024-thread latency kernel (br1024lat, default), or with TAE_B1K_LAT=0 br1024 with one
     ciphertext per workgroup and two levels per pass (or one: TAE_B1K_PAIR=0); and two ciphertexts
-    per workgroup (B > the CU count, odd tail workgroup of one): br1024s with the FFT jobs streamed
-    across the levels (default), or br1024's level-by-level kernel (TAE_B1K_STREAM=0)."""
+    per workgroup (B > the CU count, odd tail workgroup of one): br1024's level-by-level kernel (default,
+    TAE_B1K_STREAM=0) or br1024s with the FFT jobs streamed across the levels (TAE_B1K_STREAM=1)."""
     os.environ["TAE_B1K_LAT"], os.environ["TAE_B1K_PAIR"], os.environ["TAE_B1K_STREAM"] = lat, pair, stream
     try:
         ctx = tfhe_aes.context_from_raw(tfhe_aes.PARAMS_WOPPBS_8BIT, product_raw8[1], device=0)

@@ -78,6 +78,14 @@ __host__ __device__ constexpr int sidx(int q) { return SF[4 * (q & 3) + ((q >> 4
 
 constexpr int ACC_STRIDE = N;
 
+// Timing-only bound builds (garbage results; never the product): TAE_X4_HALFTW computes every twiddle /
+// twist product with 2 f64 ops instead of 4; TAE_X4_NOSWAP drops the DFT16 lane transposes entirely.
+#ifdef TAE_X4_HALFTW
+__device__ __forceinline__ cplx twmul(cplx a, cplx b) { return {fma(a.re, b.re, a.im), fma(a.im, b.im, a.re)}; }
+#else
+__device__ __forceinline__ cplx twmul(cplx a, cplx b) { return cmul(a, b); }
+#endif
+
 __device__ __forceinline__ void swap32(cplx &x, cplx &y) {
     // v_permlane32_swap: lanes 0-31 keep x and receive the partner's (lane + 32) x in y; lanes 32-63
     // receive the partner's y in x and keep y
@@ -100,13 +108,15 @@ __device__ __forceinline__ void swap32(cplx &x, cplx &y) {
 template <bool INV>
 __device__ __forceinline__ void dft16x4(cplx *v, const cplx *tw) {
     dft4<INV>(v[0], v[1], v[2], v[3]);
-    v[1] = cmul(v[1], INV ? cconj(tw[0]) : tw[0]);
-    v[2] = cmul(v[2], INV ? cconj(tw[1]) : tw[1]);
-    v[3] = cmul(v[3], INV ? cconj(tw[2]) : tw[2]);
+    v[1] = twmul(v[1], INV ? cconj(tw[0]) : tw[0]);
+    v[2] = twmul(v[2], INV ? cconj(tw[1]) : tw[1]);
+    v[3] = twmul(v[3], INV ? cconj(tw[2]) : tw[2]);
+#ifndef TAE_X4_NOSWAP
     swap32(v[0], v[2]);
     swap32(v[1], v[3]);
     swap16(v[0], v[1]);
     swap16(v[2], v[3]);
+#endif
     dft4<INV>(v[0], v[1], v[2], v[3]);
 }
 
@@ -310,14 +320,18 @@ __global__ void __launch_bounds__(THREADS, 1)
                         if (lev - 1 == l) dw = dig[l][i];
                     const double a0 = br512::lo16(dw), a1 = br512::hi16(dw);
                     const cplx tw = s_tw[ll + 64 * i];
+#ifdef TAE_X4_HALFTW
+                    v[i] = {fma(a0, tw.re, a1), fma(a1, tw.im, a0)};
+#else
                     v[i] = {fma(a0, tw.re, -(a1 * tw.im)), fma(a0, tw.im, a1 * tw.re)};
+#endif
                 }
                 dft16x4<false>(v, w16);
                 if (lev == LEV) PRIO(2);  // levels below the first keep 3 through pass A (-0.9%, same box)
 #pragma unroll
                 for (int k2 = 0; k2 < 4; k2++) {
                     const int k = r + 4 * k2;
-                    jbuf[baseA + SG3[k2]] = cmul(v[k2], s_twa[16 * k + u]);
+                    jbuf[baseA + SG3[k2]] = twmul(v[k2], s_twa[16 * k + u]);
                 }
             }
             wave_sync();
@@ -377,14 +391,14 @@ __global__ void __launch_bounds__(THREADS, 1)
 #pragma unroll
             for (int i = 0; i < 4; i++) {
                 const int kk = r + 4 * i;
-                v[i] = cmul(jbuf[baseA + SG3[i]], cconj(s_twa[16 * kk + u]));
+                v[i] = twmul(jbuf[baseA + SG3[i]], cconj(s_twa[16 * kk + u]));
             }
             dft16x4<true>(v, w16);
             uint64_t *poly = acc + jb * ACC_STRIDE;
 #pragma unroll
             for (int k2 = 0; k2 < 4; k2++) {
                 const int j = ll + 64 * k2;  // m = r + 4 k2 -> j = u + 16 m
-                const cplx t = cmul(v[k2], s_utw[j]);
+                const cplx t = twmul(v[k2], s_utw[j]);
                 bool o0, o1;
                 uint64_t a0 = torus_add_fast(t.re, poly[j], o0), a1 = torus_add_fast(t.im, poly[j + M], o1);
                 if (__builtin_amdgcn_ballot_w64(!(o0 && o1))) {  // zeros, out-of-range magnitudes (rare)

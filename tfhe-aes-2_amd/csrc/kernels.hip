@@ -766,10 +766,11 @@ void Engine::init_common() {
         // one ciphertext per 1024-thread workgroup, three levels per pass (the 8-bit model's PBS;
         // TAE_B1K_LAT=0: br1024's one-ciphertext kernel instead)
         const char *blat = getenv("TAE_B1K_LAT");
-        // two ciphertexts per workgroup with the FFT jobs streamed across the levels (the 8-bit model's PBS;
-        // TAE_B1K_STREAM=0: br1024's level-by-level kernel instead)
+        // TAE_B1K_STREAM=1: two ciphertexts per workgroup with the FFT jobs streamed across the levels
+        // (br1024s.hpp; bit-exact, but 228.7 vs 226.7 ms per 8192-ciphertext launch on one box, so br1024's
+        // level-by-level kernel stays the default; profiles/r04_ab_b1ks_sgprsel.txt)
         const char *bstr = getenv("TAE_B1K_STREAM");
-        if (p_.pbs_l == br1024s::LEV && p_.pbs_b == br1024s::BLOG && !(bstr && bstr[0] == '0')) {
+        if (p_.pbs_l == br1024s::LEV && p_.pbs_b == br1024s::BLOG && bstr && bstr[0] == '1') {
             br1024s_ = true;
             HIPC(hipFuncSetAttribute((const void *)br1024s::br_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)br1024s::lds_bytes()));
