@@ -476,6 +476,42 @@ class FFT:
         return z
 
 
+class LfTransform:
+    """The blind rotation's fused-twiddle transform for N = 512 (tfhe_oracle.c or_lf_*): forward of an
+    integer digit polynomial, backward (torus add) of a spectrum that carries the factor E2, and E2's
+    conjugate (the Fourier BSK rescale)."""
+
+    def __init__(self):
+        L = lib()
+        L.or_lf_plan_new.restype = C.c_void_p
+        L.or_lf_plan_free.argtypes = [C.c_void_p]
+        L.or_lf_fwd.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.c_void_p]
+        L.or_lf_bwd_add.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64)]
+        L.or_lf_e2.argtypes = [C.c_void_p, C.c_void_p]
+        self.h = L.or_lf_plan_new()
+
+    def __del__(self):
+        try:
+            lib().or_lf_plan_free(self.h)
+        except Exception:
+            pass
+
+    def fwd_int(self, poly: np.ndarray) -> np.ndarray:
+        out = np.zeros(256, dtype=np.complex128)
+        lib().or_lf_fwd(self.h, _pi64(np.ascontiguousarray(poly, dtype=np.int64)), out.ctypes.data_as(C.c_void_p))
+        return out
+
+    def add_bwd_torus(self, four: np.ndarray, out: np.ndarray) -> np.ndarray:
+        four = np.ascontiguousarray(four, dtype=np.complex128)
+        lib().or_lf_bwd_add(self.h, four.ctypes.data_as(C.c_void_p), _p64(out))
+        return out
+
+    def conj_e2(self) -> np.ndarray:
+        out = np.zeros(256, dtype=np.complex128)
+        lib().or_lf_e2(self.h, out.ctypes.data_as(C.c_void_p))
+        return out
+
+
 def decompose(x: int, base_log: int, levels: int):
     d = (C.c_int64 * levels)()
     lib().or_decompose(x, base_log, levels, d)

@@ -452,6 +452,199 @@ void or_fft_add_bwd_torus(const or_fft *f, const or_c64 *in, uint64_t *out) {
 }
 
 /* ======================================================================================
+ * The blind rotation's transform for N = 512 (params_sqrd_lvl_64: every CMux of the PBS; the
+ * product's br512x4 / br512lat, DESIGN.md §5.1 "fused-twiddle transform").  The same negacyclic
+ * DFT as or_fft_fwd_int / or_fft_add_bwd_torus (16 x 16 DIF, positions 16 kappa + lambda), with the
+ * arithmetic rearranged so that no twiddle is a separate complex product:
+ *  - a radix-4 stage whose 4 inputs carry unit factors w, w g, w g^2, w g^3 is evaluated relative to w
+ *    with "fused" butterflies: x + g^2 y = x + c (y + i t y) for g^2 = c (1 + i t) (Linzer-Feig), i.e.
+ *    24 fma per DFT4 instead of 3-4 complex products + 16 adds; the factor w travels to the next stage;
+ *  - the twist of the forward transform splits into lane-uniform parts (psi^64 inside the first DFT4,
+ *    whose e^{i pi/4} products act on the integer digits exactly) and factors that merge into the
+ *    following stages' ratios; the forward output is the exact DFT (no leftover factor);
+ *  - the inverse transform's input may carry any unit factor per position E2(pos) = psi^(kappa + (lambda
+ *    mod 4)): it is divided out of the Fourier BSK once (lf_rescale_bsk), and it keeps every fused ratio
+ *    off the imaginary axis (a ratio of exactly +-i has no cos-tan form).
+ * Every per-lane constant is (cos, tan) of an angle 2 pi num / 1024 from sincos2pi.  The lane programs
+ * below are the GPU's: lane (u, r) of pass A holds points j = u + 16 r + 64 i, lane (kappa, r) of pass B
+ * positions 16 kappa + r + 4 i; the transposes between the two radix-4 stages of a pass move register
+ * k of lane row r to register r of lane row k.  Bit-exact with tfhe-rs is not a goal of this transform
+ * (its FFT is not pinned either); it is pinned to the exact negacyclic product numerically
+ * (tests/test_oracle.py) and to the GPU bit for bit.
+ * ====================================================================================== */
+typedef struct {
+    double c2, t2, c1, t1; /* (cos, tan) of g^2 and of g */
+} lf4;
+typedef struct {
+    lf4 fa2[4];   /* forward pass A, stage 2, lane row k1: g = psi^16 W16^k1          (num 16 - 64 k1) */
+    lf4 fb1[16];  /* forward pass B, stage 1, lane column kappa: g = psi^4 W_M^4kappa (num 4 - 16 kappa) */
+    lf4 fb2[64];  /* forward pass B, stage 2, lane (kappa, l1): g = psi W_M^kappa W16^l1 */
+    lf4 ib2[4];   /* inverse pass B, stage 2, lane row u1: g = psi W16^-u1            (num 1 + 64 u1) */
+    lf4 ia1[16];  /* inverse pass A, stage 1, lane column u: g = psi^4 W_M^-4u        (num 4 + 16 u) */
+    lf4 ia2[64];  /* inverse pass A, stage 2, lane (u, m1): g = psi W_M^-u W16^-m1   (num 1 + 4u + 64 m1) */
+    double s2, c8, t8; /* 1/sqrt(2); cos, tan of pi/8 (psi^64) */
+    or_c64 untw[256];  /* conj(twist[j]); the backward 2^-8 is exact and applied to the sum */
+    or_c64 e2[256];    /* conj(E2(pos)): the Fourier BSK rescale */
+} lf_plan;
+
+static void lf_ct(long num, double *c, double *t) {
+    double s;
+    sincos2pi(num, 1024, c, &s);
+    *t = s / *c;
+}
+static void lf_make(long num, lf4 *o) {
+    lf_ct(2 * num, &o->c2, &o->t2);
+    lf_ct(num, &o->c1, &o->t1);
+}
+
+static void or_lf_plan_build(lf_plan *P) {
+    for (int k = 0; k < 4; k++) {
+        lf_make(16 - 64 * k, &P->fa2[k]);
+        lf_make(1 + 64 * k, &P->ib2[k]);
+    }
+    for (int a = 0; a < 16; a++) {
+        lf_make(4 - 16 * a, &P->fb1[a]);
+        lf_make(4 + 16 * a, &P->ia1[a]);
+        for (int l = 0; l < 4; l++) {
+            lf_make(1 - 4 * a - 64 * l, &P->fb2[4 * a + l]);
+            lf_make(1 + 4 * a + 64 * l, &P->ia2[4 * a + l]);
+        }
+    }
+    double c, s;
+    P->s2 = 1.0 / sqrt(2.0);
+    lf_ct(64, &P->c8, &P->t8);
+    for (int j = 0; j < 256; j++) {
+        sincos2pi(j, 1024, &c, &s);
+        P->untw[j].re = c;
+        P->untw[j].im = -s;
+        sincos2pi(-((j >> 4) + (j & 3)), 1024, &c, &s);
+        P->e2[j].re = c;
+        P->e2[j].im = s;
+    }
+}
+
+/* x -> x (1 + i t) */
+static inline or_c64 lf_rot(or_c64 x, double t) { return (or_c64){fma(-t, x.im, x.re), fma(t, x.re, x.im)}; }
+static inline or_c64 lf_add(or_c64 a, double c, or_c64 t) { return (or_c64){fma(c, t.re, a.re), fma(c, t.im, a.im)}; }
+
+/* DFT4 (W4 = -i forward, +i inverse) of x0, g x1, g^2 x2, g^3 x3, relative to x0's factor */
+static void lf_dft4(const or_c64 *x, const lf4 *K, int inv, or_c64 *y) {
+    or_c64 t = lf_rot(x[2], K->t2), s = lf_rot(x[3], K->t2);
+    or_c64 u0 = lf_add(x[0], K->c2, t), u1 = lf_add(x[0], -K->c2, t);
+    or_c64 v0 = lf_add(x[1], K->c2, s), v1 = lf_add(x[1], -K->c2, s);
+    or_c64 p = lf_rot(v0, K->t1), q = lf_rot(v1, K->t1);
+    y[0] = lf_add(u0, K->c1, p);
+    y[2] = lf_add(u0, -K->c1, p);
+    /* u1 -/+ i c1 q: (u1.re +/- c1 q.im, u1.im -/+ c1 q.re) */
+    double c = inv ? -K->c1 : K->c1;
+    y[1] = (or_c64){fma(c, q.im, u1.re), fma(-c, q.re, u1.im)};
+    y[3] = (or_c64){fma(-c, q.im, u1.re), fma(c, q.re, u1.im)};
+}
+
+/* forward transform of one digit polynomial (N = 512 integers) into X[16 kappa + lambda] */
+void or_lf_fwd(const void *plan, const int64_t *poly, or_c64 *X) {
+    const lf_plan *P = (const lf_plan *)plan;
+    or_c64 Q[16][4][4]; /* [u][r][k1] */
+    or_c64 z[256];
+    for (int u = 0; u < 16; u++)
+        for (int r = 0; r < 4; r++) {
+            double d0r, d0i, d1r, d1i, p2r, p2i, p3r, p3i;
+            int64_t d[4][2];
+            for (int i = 0; i < 4; i++) {
+                int j = u + 16 * r + 64 * i;
+                d[i][0] = poly[j];
+                d[i][1] = poly[j + 256];
+            }
+            d0r = (double)d[0][0], d0i = (double)d[0][1], d1r = (double)d[1][0], d1i = (double)d[1][1];
+            p2r = (double)(d[2][0] - d[2][1]), p2i = (double)(d[2][0] + d[2][1]);
+            p3r = (double)(d[3][0] - d[3][1]), p3i = (double)(d[3][0] + d[3][1]);
+            or_c64 Ep = {fma(P->s2, p2r, d0r), fma(P->s2, p2i, d0i)}, Em = {fma(-P->s2, p2r, d0r), fma(-P->s2, p2i, d0i)};
+            or_c64 Op = {fma(P->s2, p3r, d1r), fma(P->s2, p3i, d1i)}, Om = {fma(-P->s2, p3r, d1r), fma(-P->s2, p3i, d1i)};
+            or_c64 a = lf_rot(Op, P->t8), b = lf_rot(Om, P->t8);
+            Q[u][r][0] = lf_add(Ep, P->c8, a);
+            Q[u][r][2] = lf_add(Ep, -P->c8, a);
+            Q[u][r][1] = (or_c64){fma(P->c8, b.im, Em.re), fma(-P->c8, b.re, Em.im)};
+            Q[u][r][3] = (or_c64){fma(-P->c8, b.im, Em.re), fma(P->c8, b.re, Em.im)};
+        }
+    for (int u = 0; u < 16; u++)
+        for (int k1 = 0; k1 < 4; k1++) {
+            or_c64 x[4], y[4];
+            for (int r = 0; r < 4; r++) x[r] = Q[u][r][k1];
+            lf_dft4(x, &P->fa2[k1], 0, y);
+            for (int k2 = 0; k2 < 4; k2++) z[u + 16 * (k1 + 4 * k2)] = y[k2];
+        }
+    or_c64 R[16][4][4]; /* [kappa][r][l1] */
+    for (int a = 0; a < 16; a++)
+        for (int r = 0; r < 4; r++) {
+            or_c64 x[4];
+            for (int i = 0; i < 4; i++) x[i] = z[(r + 4 * i) + 16 * a];
+            lf_dft4(x, &P->fb1[a], 0, R[a][r]);
+        }
+    for (int a = 0; a < 16; a++)
+        for (int l1 = 0; l1 < 4; l1++) {
+            or_c64 x[4], y[4];
+            for (int r = 0; r < 4; r++) x[r] = R[a][r][l1];
+            lf_dft4(x, &P->fb2[4 * a + l1], 0, y);
+            for (int l2 = 0; l2 < 4; l2++) X[16 * a + l1 + 4 * l2] = y[l2];
+        }
+}
+
+/* backward transform of Y[16 kappa + lambda] (which carries the factor E2) added to the torus
+ * polynomial out (N = 512): untwist conj(twist), 2^-8 exact, from_torus */
+void or_lf_bwd_add(const void *plan, const or_c64 *Y, uint64_t *out) {
+    const lf_plan *P = (const lf_plan *)plan;
+    or_c64 R[16][4][4]; /* [kappa][r][u1] */
+    or_c64 z[256];
+    for (int a = 0; a < 16; a++)
+        for (int r = 0; r < 4; r++) {
+            or_c64 v[4];
+            for (int i = 0; i < 4; i++) v[i] = Y[16 * a + r + 4 * i];
+            dft4(v, 0, 1, 1);
+            for (int k = 0; k < 4; k++) R[a][r][k] = v[k];
+        }
+    for (int a = 0; a < 16; a++)
+        for (int u1 = 0; u1 < 4; u1++) {
+            or_c64 x[4], y[4];
+            for (int r = 0; r < 4; r++) x[r] = R[a][r][u1];
+            lf_dft4(x, &P->ib2[u1], 1, y);
+            for (int u2 = 0; u2 < 4; u2++) z[16 * a + u1 + 4 * u2] = y[u2];
+        }
+    or_c64 S[16][4][4]; /* [u][r][m1] */
+    for (int u = 0; u < 16; u++)
+        for (int r = 0; r < 4; r++) {
+            or_c64 x[4];
+            for (int i = 0; i < 4; i++) x[i] = z[u + 16 * (r + 4 * i)];
+            lf_dft4(x, &P->ia1[u], 1, S[u][r]);
+        }
+    for (int u = 0; u < 16; u++)
+        for (int m1 = 0; m1 < 4; m1++) {
+            or_c64 x[4], y[4];
+            for (int r = 0; r < 4; r++) x[r] = S[u][r][m1];
+            lf_dft4(x, &P->ia2[4 * u + m1], 1, y);
+            for (int m2 = 0; m2 < 4; m2++) {
+                int j = u + 16 * (m1 + 4 * m2);
+                or_c64 t = cmul(y[m2], P->untw[j]);
+                out[j] += or_from_torus(t.re * 0x1p-8);
+                out[j + 256] += or_from_torus(t.im * 0x1p-8);
+            }
+        }
+}
+
+void *or_lf_plan_new(void) {
+    lf_plan *P = (lf_plan *)malloc(sizeof(lf_plan));
+    or_lf_plan_build(P);
+    return P;
+}
+void or_lf_plan_free(void *plan) { free(plan); }
+void or_lf_e2(const void *plan, or_c64 *e2) { memcpy(e2, ((const lf_plan *)plan)->e2, sizeof(or_c64) * 256); }
+
+/* the Fourier BSK the fused transform multiplies with: G * conj(E2(pos)) per position */
+static void lf_rescale(const lf_plan *P, or_c64 *G, size_t polys) {
+    for (size_t i = 0; i < polys; i++)
+        for (int f = 0; f < 256; f++) G[i * 256 + f] = cmul(G[i * 256 + f], P->e2[f]);
+}
+
+/* ======================================================================================
  * GLWE / LWE encryption (tfhe-rs encrypt_lwe_ciphertext / encrypt_glwe_ciphertext), with
  * the keygen randomness spec of DESIGN.md: ciphertext #idx of purpose P draws its mask from
  * ChaCha20(seed, nonce = 2P | (idx >> 40) << 8, ctr = (idx mod 2^40) * 2^24) and its noise from
@@ -580,6 +773,10 @@ static void *kg_worker(void *arg) {
     return NULL;
 }
 
+/* the parameter sets whose blind rotation runs the fused-twiddle transform (the product's br512x4 /
+ * br512lat shape: N = 512, k = 4, 3 levels of 2^12 = params_sqrd_lvl_64) */
+static int lf_set(const or_params *p) { return p->N == 512 && p->k == 4 && p->pbs_l == 3 && p->pbs_b == 12; }
+
 static void server_key_fourier(or_server_key *sk) {
     const or_params *p = &sk->p;
     int M = p->N / 2;
@@ -587,6 +784,11 @@ static void server_key_fourier(or_server_key *sk) {
     sk->bsk_f = (or_c64 *)malloc(sizeof(or_c64) * polys * M);
     for (size_t i = 0; i < polys; i++)
         or_fft_fwd_torus(sk->fft, sk->bsk + i * p->N, sk->bsk_f + i * M);
+    sk->lf = NULL;
+    if (lf_set(p)) {
+        sk->lf = or_lf_plan_new();
+        lf_rescale((const lf_plan *)sk->lf, sk->bsk_f, polys);
+    }
 }
 
 /* shortint_woppbs_1bit.rs:245-268 (gen_keys + new_wopbs_key_only_for_wopbs) */
@@ -658,6 +860,7 @@ void or_server_key_free(or_server_key *sk) {
     free(sk->pfpksk);
     free(sk->bsk_f);
     or_fft_free(sk->fft);
+    or_lf_plan_free(sk->lf);
     free(sk);
 }
 
@@ -726,8 +929,17 @@ void or_keyswitch(const or_server_key *sk, const uint64_t *in, uint64_t *out) {
 /* fft64::crypto::ggsw::add_external_product_assign.  Fourier GGSW layout
  * [lev-1][row p][col c][M]; levels are consumed finest first (ggsw.into_levels().rev() zipped
  * with the decomposition iterator), rows in order; the f64 MAC is the fixed fma sequence below. */
+static void ext_product_add(const or_server_key *sk, const void *lf, const or_c64 *ggsw, int levels, int base_log,
+                            const uint64_t *in, uint64_t *out);
 void or_external_product_add(const or_server_key *sk, const or_c64 *ggsw, int levels, int base_log,
                              const uint64_t *in, uint64_t *out) {
+    ext_product_add(sk, NULL, ggsw, levels, base_log, in, out);
+}
+
+/* lf != NULL: the blind rotation's external product with the fused-twiddle transform (ggsw = a BSK
+ * element of the rescaled Fourier BSK) */
+static void ext_product_add(const or_server_key *sk, const void *lf, const or_c64 *ggsw, int levels, int base_log,
+                            const uint64_t *in, uint64_t *out) {
     const or_params *p = &sk->p;
     int k = p->k, N = p->N, M = N / 2;
     size_t glwe = (size_t)(k + 1) * N;
@@ -743,7 +955,10 @@ void or_external_product_add(const or_server_key *sk, const or_c64 *ggsw, int le
     for (int lev = levels; lev >= 1; lev--) {
         for (int r = 0; r <= k; r++) {
             memcpy(poly, dig + (size_t)(lev - 1) * glwe + (size_t)r * N, sizeof(int64_t) * N);
-            or_fft_fwd_int(sk->fft, poly, X);
+            if (lf)
+                or_lf_fwd(lf, poly, X);
+            else
+                or_fft_fwd_int(sk->fft, poly, X);
             for (int c = 0; c <= k; c++) {
                 const or_c64 *G = ggsw + (((size_t)(lev - 1) * (k + 1) + r) * (k + 1) + c) * M;
                 or_c64 *A = acc + (size_t)c * M;
@@ -759,7 +974,12 @@ void or_external_product_add(const or_server_key *sk, const or_c64 *ggsw, int le
             }
         }
     }
-    for (int c = 0; c <= k; c++) or_fft_add_bwd_torus(sk->fft, acc + (size_t)c * M, out + (size_t)c * N);
+    for (int c = 0; c <= k; c++) {
+        if (lf)
+            or_lf_bwd_add(lf, acc + (size_t)c * M, out + (size_t)c * N);
+        else
+            or_fft_add_bwd_torus(sk->fft, acc + (size_t)c * M, out + (size_t)c * N);
+    }
     free(dig);
     free(acc);
     free(X);
@@ -800,7 +1020,8 @@ void or_bootstrap(const or_server_key *sk, const uint64_t *lwe_in, const uint64_
         if (lwe_in[i] == 0) continue;
         int64_t at = (int64_t)or_pbs_modulus_switch(lwe_in[i], N);
         for (int c = 0; c <= k; c++) or_monomial_mul(acc + (size_t)c * N, ct1 + (size_t)c * N, N, at);
-        or_cmux(sk, acc, ct1, sk->bsk_f + (size_t)i * ggsw_sz, p->pbs_l, p->pbs_b);
+        for (size_t t = 0; t < glwe; t++) ct1[t] -= acc[t];  /* cmux: acc += ggsw [x] (ct1 - acc) */
+        ext_product_add(sk, sk->lf, sk->bsk_f + (size_t)i * ggsw_sz, p->pbs_l, p->pbs_b, ct1, acc);
     }
     sample_extract(acc, k, N, lwe_out);
     free(acc);

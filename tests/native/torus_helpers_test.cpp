@@ -30,6 +30,16 @@ static void check_ft(double x) {
         if (fails++ < 10) printf("torus_add_fast(%a): ok %d got %016llx want %016llx\n", x, (int)ok,
                                  (unsigned long long)(acc - acc0), (unsigned long long)b);
     }
+    // the fused transform's conversion of y = x 2^8 (lf512.hpp: the untwist's exact 2^-8 folded into the
+    // exponent) equals the conversion of x whenever it accepts y
+    {
+        const double y = x * 0x1p8;
+        bool ok8;
+        const uint64_t a8 = tae::torus_add_fast_sh<8>(y, acc0, ok8);
+        if ((ok8 != ok || (ok8 && a8 != acc)) && fails++ < 10)
+            printf("torus_add_fast_sh<8>(%a): ok %d got %016llx want %016llx\n", y, (int)ok8,
+                   (unsigned long long)(a8 - acc0), (unsigned long long)b);
+    }
     // the kernels' fallback undoes the fast value (linear in acc) and adds the exact one
     bool d;
     if (acc - tae::torus_add_fast(x, 0, d) + b != acc0 + b && fails++ < 10)

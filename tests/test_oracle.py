@@ -58,6 +58,49 @@ def test_fft_negacyclic_product_within_bound(oracle_mod, N):
         assert np.max(np.abs(err)) < 2**32
 
 
+def test_lf_transform_is_the_negacyclic_dft(oracle_mod):
+    """The blind rotation's fused-twiddle transform (N = 512) computes the same negacyclic
+    DFT as the radix-16 schedule: forward of digit polynomials within 1e-15 relative of it, both within
+    1e-12 of the definition sum; and it has no output factor."""
+    F, T = oracle_mod.FFT(512), oracle_mod.LfTransform()
+    rng = np.random.default_rng(11)
+    j = np.arange(256)
+    pos = np.arange(256)
+    W = np.exp(1j * np.pi * j / 512)[None, :] * np.exp(
+        -2j * np.pi * np.outer((pos >> 4) + 16 * (pos & 15), j) / 256)
+    for _ in range(5):
+        d = rng.integers(-2048, 2049, size=512).astype(np.int64)
+        x_lf, x_std = T.fwd_int(d), F.fwd_int(d)
+        exact = W @ (d[:256] + 1j * d[256:])
+        scale = np.max(np.abs(exact))
+        assert np.max(np.abs(x_lf - x_std)) / scale < 1e-15
+        assert np.max(np.abs(x_lf - exact)) / scale < 1e-12
+
+
+def test_lf_negacyclic_product_within_bound(oracle_mod):
+    """The fused transform's external-product arithmetic against the exact negacyclic product mod 2^64 with
+    the BSK-side spectrum times conj(E2) (what the rescaled Fourier BSK holds): the same 2^32 bound as the
+    radix-16 schedule (test_fft_negacyclic_product_within_bound), and a round trip as tight as its."""
+    F, T = oracle_mod.FFT(512), oracle_mod.LfTransform()
+    e2 = T.conj_e2()
+    assert np.allclose(np.abs(e2), 1.0)
+    rng = np.random.default_rng(12)
+    for _ in range(3):
+        a = rng.integers(0, 2**64 - 1, size=512, dtype=np.uint64)
+        b = rng.integers(-2048, 2049, size=512).astype(np.int64)
+        exact = oracle_mod.negacyclic_mul_exact(a, b)
+        out = np.zeros(512, dtype=np.uint64)
+        T.add_bwd_torus(F.fwd_torus(a) * e2 * T.fwd_int(b), out)
+        err = (out - exact).astype(np.int64)
+        assert np.max(np.abs(err)) < 2**32
+        rt_lf, rt_std = np.zeros(512, dtype=np.uint64), np.zeros(512, dtype=np.uint64)
+        T.add_bwd_torus(F.fwd_torus(a) * e2, rt_lf)
+        F.add_bwd_torus(F.fwd_torus(a), rt_std)
+        e_lf = np.max(np.abs((rt_lf - a).astype(np.int64)))
+        e_std = np.max(np.abs((rt_std - a).astype(np.int64)))
+        assert e_lf < 4 * max(e_std, 1) and e_lf < 2**16
+
+
 def test_generate_luts_exact_layout(oracle_mod, golden):
     """shortint_woppbs_1bit.rs:665-697 (vertical packing and multi-polynomial LUT layout)."""
     lut = oracle_mod.generate_lut(16, 3, 2, lambda v: v)

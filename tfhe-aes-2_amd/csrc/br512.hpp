@@ -51,6 +51,31 @@ __device__ __forceinline__ void swap16(cplx &x, cplx &y) {
     __builtin_memcpy(&y, &b, 16);
 }
 
+__device__ __forceinline__ void swap32(cplx &x, cplx &y) {
+    // v_permlane32_swap: lanes 0-31 keep x and receive the partner's (lane + 32) x in y; lanes 32-63
+    // receive the partner's y in x and keep y
+    u32x4 a, b;
+    __builtin_memcpy(&a, &x, 16);
+    __builtin_memcpy(&b, &y, 16);
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        const auto r = __builtin_amdgcn_permlane32_swap(a[w], b[w], false, false);
+        a[w] = r[0];
+        b[w] = r[1];
+    }
+    __builtin_memcpy(&x, &a, 16);
+    __builtin_memcpy(&y, &b, 16);
+}
+
+// 4 x 4 transpose over the lane rows (lanes u, u+16, u+32, u+48) of a DFT16 job: register k of lane
+// row r moves to register r of lane row k
+__device__ __forceinline__ void transpose4(cplx *v) {
+    swap32(v[0], v[2]);
+    swap32(v[1], v[3]);
+    swap16(v[0], v[1]);
+    swap16(v[2], v[3]);
+}
+
 __device__ __forceinline__ double lo16(uint32_t w) { return (double)((int32_t)(w << 16) >> 16); }
 __device__ __forceinline__ double hi16(uint32_t w) { return (double)((int32_t)w >> 16); }
 

@@ -65,18 +65,16 @@ template <int LEV, int BLOG>
 __global__ void __launch_bounds__(THREADS, 1)
     br_kernel(const uint64_t *__restrict__ lwe_in, int n, const uint64_t *__restrict__ lut,
               const cplx *__restrict__ bsk, uint64_t *__restrict__ out, long B, uint64_t body_add,
-              uint64_t out_add, const cplx *__restrict__ twist, const cplx *__restrict__ wtab) {
+              uint64_t out_add, const double *__restrict__ lf) {
     static_assert(LEV * K1 <= THREADS / 64, "one wave per (level, polynomial) job");
     constexpr int LOGN = 9, JOBS = LEV * K1;
     extern __shared__ __align__(16) unsigned char smem[];
     uint64_t *acc = reinterpret_cast<uint64_t *>(smem);             // [K1][N]
     cplx *buf = reinterpret_cast<cplx *>(acc + K1 * N);             // [JOBS][BUF_STRIDE] spectra
     cplx *obuf = buf + JOBS * BUF_STRIDE;                           // [K1][BUF_STRIDE] MAC results
-    cplx *s_tw = obuf + K1 * BUF_STRIDE;                            // twist e^{i pi j / N}
-    cplx *s_twa = s_tw + M;                                         // [16 a + b] = W_M^{a b}
-    cplx *s_utw = s_twa + M;                                        // conj(twist) 2^-8 (exact)
-    cplx *s_w16 = s_utw + M;                                        // [r][3]: W16^{r k1}
-    uint32_t *s_dig = reinterpret_cast<uint32_t *>(s_w16 + 12);     // [LEV][K1][N/2] packed digit pairs
+    double *s_lf = reinterpret_cast<double *>(obuf + K1 * BUF_STRIDE);  // the fused transform's table (lf512.hpp)
+    const cplx *s_untw = reinterpret_cast<const cplx *>(s_lf + lf512::UNTW);
+    uint32_t *s_dig = reinterpret_cast<uint32_t *>(s_lf + lf512::KERNEL_DOUBLES);  // [LEV][K1][N/2] packed digit pairs
     const long ct = blockIdx.x;
     if (ct >= B) return;  // whole workgroup
     const int tid = threadIdx.x;
@@ -86,17 +84,8 @@ __global__ void __launch_bounds__(THREADS, 1)
     const int jlev = fjob ? jb / K1 + 1 : 1, jp = fjob ? jb - (jb / K1) * K1 : 0;
     const uint64_t *in = lwe_in + (size_t)ct * (n + 1);
 
-    for (int t = tid; t < M; t += THREADS) {
-        s_tw[t] = twist[t];
-        s_twa[t] = wtab[(t >> 4) * (t & 15)];
-        s_utw[t] = cplx{twist[t].re * 0x1p-8, -twist[t].im * 0x1p-8};
-    }
-    if (tid < 12) {
-        const int rr = tid / 3, k1 = tid - 3 * rr + 1;
-        const int e = (rr * k1) & 15;
-        const cplx w = wtab[16 * e];
-        s_w16[tid] = e == 0 ? cplx{1.0, 0.0} : (e == 4 ? cplx{0.0, -1.0} : w);
-    }
+    for (int t = tid; t < lf512::KERNEL_DOUBLES; t += THREADS) s_lf[t] = lf[t];
+    const double lf_s2 = lf[lf512::CONSTS], lf_c8 = lf[lf512::CONSTS + 1], lf_t8 = lf[lf512::CONSTS + 2];
     {
         const int bt = mod_switch(in[n] + body_add, LOGN);
         const int e0 = (2 * N - (bt % (2 * N))) % (2 * N);
@@ -115,7 +104,6 @@ __global__ void __launch_bounds__(THREADS, 1)
     const int baseA = SF[4 * (u & 3) + r] + SG1[u >> 2], baseB = SF[4 * r + (u & 3)] + SG3[u >> 2];
     const bool two = tid < M;
     const int goff = pos * (int)sizeof(cplx);
-    const cplx *my_w16 = s_w16 + 3 * r;
     int ll = lane;
     asm volatile("" : "+v"(ll));
 
@@ -177,30 +165,24 @@ __global__ void __launch_bounds__(THREADS, 1)
 #pragma unroll
             for (int p = 0; p < K1; p++) gb[p] = gload(gstep, LEV, p, K1 - 1, false);
         }
-        if (fjob) {
+        if (fjob) {  // the fused-twiddle transform (lf512.hpp), as br512x4's PBS mode
             cplx *dst = buf + jb * BUF_STRIDE;
-            cplx w16[3];  // read once for passes A and B
+            uint32_t dw[4];
 #pragma unroll
-            for (int k = 0; k < 3; k++) w16[k] = my_w16[k];
+            for (int i = 0; i < 4; i++) dw[i] = s_dig[((jlev - 1) * K1 + jp) * M + ll + 64 * i];
             cplx v[4];
+            lf512::a1(dw, v, lf_s2, lf_c8, lf_t8);
+            br512::transpose4(v);
+            lf512::dft4<false>(v, lf512::k4(s_lf, lf512::FA2 + 4 * r));
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const uint32_t d = s_dig[((jlev - 1) * K1 + jp) * M + ll + 64 * i];
-                const double a0 = br512::lo16(d), a1 = br512::hi16(d);
-                const cplx tw = s_tw[ll + 64 * i];
-                v[i] = {fma(a0, tw.re, -(a1 * tw.im)), fma(a0, tw.im, a1 * tw.re)};
-            }
-            dft16x4<false>(v, w16);
-#pragma unroll
-            for (int k2 = 0; k2 < 4; k2++) {
-                const int kq = r + 4 * k2;
-                dst[baseA + SG3[k2]] = cmul(v[k2], s_twa[16 * kq + u]);
-            }
+            for (int k2 = 0; k2 < 4; k2++) dst[baseA + SG3[k2]] = v[k2];
             wave_sync();
-            // pass B (row u): DFT16 over positions 16 u + r + 4 i, in place
+            // pass B (row kappa = u): positions 16 u + r + 4 i, in place
 #pragma unroll
             for (int i = 0; i < 4; i++) v[i] = dst[baseB + SG1[i]];
-            dft16x4<false>(v, w16);
+            lf512::dft4<false>(v, lf512::k4(s_lf, lf512::FB1 + 4 * u));
+            br512::transpose4(v);
+            lf512::dft4<false>(v, lf512::k4(s_lf, lf512::FB2 + 4 * (4 * u + r)));
 #pragma unroll
             for (int k2 = 0; k2 < 4; k2++) dst[baseB + SG1[k2]] = v[k2];
         }
@@ -247,22 +229,20 @@ __global__ void __launch_bounds__(THREADS, 1)
         // other waves) ----
         if (jb < K1) {
             cplx *base = obuf + jb * BUF_STRIDE;
-            cplx w16[3];  // read once for both inverse passes
-#pragma unroll
-            for (int k = 0; k < 3; k++) w16[k] = my_w16[k];
             cplx v[4];
 #pragma unroll
             for (int i = 0; i < 4; i++) v[i] = base[baseB + SG1[i]];
-            dft16x4<true>(v, w16);
+            dft4<true>(v[0], v[1], v[2], v[3]);
+            br512::transpose4(v);
+            lf512::dft4<true>(v, lf512::k4(s_lf, lf512::IB2 + 4 * r));
 #pragma unroll
             for (int k2 = 0; k2 < 4; k2++) base[baseB + SG1[k2]] = v[k2];
             wave_sync();
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const int kk = r + 4 * i;
-                v[i] = cmul(base[baseA + SG3[i]], cconj(s_twa[16 * kk + u]));
-            }
-            dft16x4<true>(v, w16);
+            for (int i = 0; i < 4; i++) v[i] = base[baseA + SG3[i]];
+            lf512::dft4<true>(v, lf512::k4(s_lf, lf512::IA1 + 4 * u));
+            br512::transpose4(v);
+            lf512::dft4<true>(v, lf512::k4(s_lf, lf512::IA2 + 4 * (4 * u + r)));
             wave_sync();  // this wave's reads of base precede its writes below (LDS executes in order)
 #pragma unroll
             for (int k2 = 0; k2 < 4; k2++) base[ll + 64 * k2] = v[k2];  // coefficient pair j = ll + 64 k2
@@ -283,13 +263,13 @@ __global__ void __launch_bounds__(THREADS, 1)
         // ---- I2: untwist, torus conversion, ACC += over all waves: item t = (q, j) ----
         for (int t = tid; t < K1 * M; t += THREADS) {
             const int q = t >> 8, j = t & (M - 1);  // wave-uniform q (64 consecutive j)
-            const cplx x = cmul(obuf[q * BUF_STRIDE + j], s_utw[j]);
+            const cplx x = cmul(obuf[q * BUF_STRIDE + j], s_untw[j]);  // x 2^-8 (exact) in the conversion
             uint64_t *poly = acc + q * N;
             bool o0, o1;
-            uint64_t a0 = torus_add_fast(x.re, poly[j], o0), a1 = torus_add_fast(x.im, poly[j + M], o1);
+            uint64_t a0 = torus_add_fast_sh<8>(x.re, poly[j], o0), a1 = torus_add_fast_sh<8>(x.im, poly[j + M], o1);
             if (__builtin_amdgcn_ballot_w64(!(o0 && o1))) {  // zeros, out-of-range magnitudes (rare)
-                a0 = poly[j] + from_torus_bits(x.re);
-                a1 = poly[j + M] + from_torus_bits(x.im);
+                a0 = poly[j] + from_torus_bits(x.re * 0x1p-8);
+                a1 = poly[j + M] + from_torus_bits(x.im * 0x1p-8);
             }
             poly[j] = a0;
             poly[j + M] = a1;
@@ -316,7 +296,7 @@ __global__ void __launch_bounds__(THREADS, 1)
 }
 
 inline size_t lds_bytes(int lev) {
-    return (size_t)K1 * N * 8 + (size_t)(lev * K1 + K1) * BUF_STRIDE * 16 + 3 * (size_t)M * 16 + 12 * 16 +
+    return (size_t)K1 * N * 8 + (size_t)(lev * K1 + K1) * BUF_STRIDE * 16 + (size_t)lf512::KERNEL_DOUBLES * 8 +
            (size_t)lev * K1 * M * 4;
 }
 

@@ -20,6 +20,7 @@
 // 64 consecutive coefficients.
 #pragma once
 #include "br512.hpp"
+#include "lf512.hpp"
 
 namespace tae {
 namespace br512x4 {
@@ -29,6 +30,7 @@ using br512::lds_sync;
 using br512::M;
 using br512::N;
 using br512::swap16;
+using br512::swap32;
 using br512::u32x4;
 using br512::wave_sync;
 
@@ -85,22 +87,6 @@ __device__ __forceinline__ cplx twmul(cplx a, cplx b) { return {fma(a.re, b.re, 
 #else
 __device__ __forceinline__ cplx twmul(cplx a, cplx b) { return cmul(a, b); }
 #endif
-
-__device__ __forceinline__ void swap32(cplx &x, cplx &y) {
-    // v_permlane32_swap: lanes 0-31 keep x and receive the partner's (lane + 32) x in y; lanes 32-63
-    // receive the partner's y in x and keep y
-    u32x4 a, b;
-    __builtin_memcpy(&a, &x, 16);
-    __builtin_memcpy(&b, &y, 16);
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-        const auto r = __builtin_amdgcn_permlane32_swap(a[w], b[w], false, false);
-        a[w] = r[0];
-        b[w] = r[1];
-    }
-    __builtin_memcpy(&x, &a, 16);
-    __builtin_memcpy(&y, &b, 16);
-}
 
 // DFT16 over the lanes (u, 0..3) of a row group: in v[i] = x[r + 4 i], out v[k2] = X[r + 4 k2];
 // tw[k1 - 1] = W16^{r k1} (forward values).  Stage-1 outputs M[r][k1] are transposed to
@@ -164,7 +150,7 @@ __global__ void __launch_bounds__(THREADS, 1)
     br_kernel(const uint64_t *__restrict__ lwe_in, int n, const uint64_t *__restrict__ lut, int n_out,
               const cplx *__restrict__ ggsw_base, int n_in, uint64_t *__restrict__ out, long B,
               uint64_t body_add, uint64_t out_add, const cplx *__restrict__ twist, const cplx *__restrict__ wtab,
-              uint64_t *__restrict__ clk) {
+              const double *__restrict__ lf, uint64_t *__restrict__ clk) {
     constexpr int LOGN = 9;
     ClockStamp stamp;
     stamp.start(clk);
@@ -175,6 +161,9 @@ __global__ void __launch_bounds__(THREADS, 1)
     cplx *s_twa = s_tw + M;                                         // [16 a + b] = W_M^{a b}
     cplx *s_utw = s_twa + M;                                        // conj(twist) 2^-8 (exact)
     cplx *s_w16 = s_utw + M;                                        // [r][3]: W16^{r k1}, k1 = 1..3
+    // PBS mode: the fused-twiddle transform's table (lf512.hpp) in place of the four tables above
+    double *s_lf = reinterpret_cast<double *>(s_tw);
+    const cplx *s_untw = reinterpret_cast<const cplx *>(s_lf + lf512::UNTW);
     const int tid = threadIdx.x;
     const int jb = __builtin_amdgcn_readfirstlane(tid >> 6);  // job = wave
     const int lane = tid & 63, u = lane & 15, r = lane >> 4;
@@ -195,12 +184,23 @@ __global__ void __launch_bounds__(THREADS, 1)
     }
     const bool jvalid = fjob && jct < nct;
 
-    for (int t = tid; t < M; t += THREADS) {
-        s_tw[t] = twist[t];
-        s_twa[t] = wtab[(t >> 4) * (t & 15)];
-        s_utw[t] = cplx{twist[t].re * 0x1p-8, -twist[t].im * 0x1p-8};
+    if constexpr (PBS) {
+        for (int t = tid; t < lf512::KERNEL_DOUBLES; t += THREADS) s_lf[t] = lf[t];
+    } else {
+        for (int t = tid; t < M; t += THREADS) {
+            s_tw[t] = twist[t];
+            s_twa[t] = wtab[(t >> 4) * (t & 15)];
+            s_utw[t] = cplx{twist[t].re * 0x1p-8, -twist[t].im * 0x1p-8};
+        }
     }
-    if (tid < 12) {
+    // lane-uniform constants of the fused transform's first stage (scalar registers)
+    double lf_s2 = 0, lf_c8 = 0, lf_t8 = 0;
+    if constexpr (PBS) {
+        lf_s2 = lf[lf512::CONSTS];
+        lf_c8 = lf[lf512::CONSTS + 1];
+        lf_t8 = lf[lf512::CONSTS + 2];
+    }
+    if (!PBS && tid < 12) {
         // s_w16[3 r + k1 - 1] = W16^{r k1} = W_M^{16 e}, e = r k1 mod 16; exact 1 and -i for e = 0, 4
         const int rr = tid / 3, k1 = tid - 3 * rr + 1;
         const int e = (rr * k1) & 15;
@@ -304,6 +304,42 @@ __global__ void __launch_bounds__(THREADS, 1)
 #pragma unroll
         for (int lev = LEV; lev >= 1; lev--) {
             load_level(lev);
+            if constexpr (PBS) {
+                // fused-twiddle transform (lf512.hpp): pass A = DFT4 of the twisted digits, transpose, fused
+                // DFT4 -> LDS position u + 16 k (its W_M^{u k} and psi^u factors ride into pass B)
+                if (fjob) {
+                    uint32_t dw[4];
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        dw[i] = dig[0][i];
+#pragma unroll
+                        for (int l = 1; l < LEV; l++)
+                            if (lev - 1 == l) dw[i] = dig[l][i];
+                    }
+                    cplx v[4];
+                    lf512::a1(dw, v, lf_s2, lf_c8, lf_t8);
+                    br512::transpose4(v);
+                    lf512::dft4<false>(v, lf512::k4(s_lf, lf512::FA2 + 4 * r));
+                    if (lev == LEV) PRIO(2);
+#pragma unroll
+                    for (int k2 = 0; k2 < 4; k2++) jbuf[baseA + SG3[k2]] = v[k2];
+                }
+                wave_sync();
+                PRIO(1);
+                PROF_T(1);
+                // pass B (row kappa = u): fused DFT4 over the columns r + 4 i, transpose, fused DFT4, in place
+                if (fjob) {
+                    cplx v[4];
+#pragma unroll
+                    for (int i = 0; i < 4; i++) v[i] = jbuf[baseB + SG1[i]];
+                    lf512::dft4<false>(v, lf512::k4(s_lf, lf512::FB1 + 4 * u));
+                    br512::transpose4(v);
+                    lf512::dft4<false>(v, lf512::k4(s_lf, lf512::FB2 + 4 * (4 * u + r)));
+                    PRIO(0);
+#pragma unroll
+                    for (int k2 = 0; k2 < 4; k2++) jbuf[baseB + SG1[k2]] = v[k2];
+                }
+            } else {
             // the lane's W16 factors, read once for passes A and B (dead before the MAC, so they do
             // not add to its register peak): 3 of the 11 LDS reads of pass B's LDS-bound phase
             cplx w16[3];
@@ -347,6 +383,7 @@ __global__ void __launch_bounds__(THREADS, 1)
 #pragma unroll
                 for (int k2 = 0; k2 < 4; k2++) jbuf[baseB + SG1[k2]] = v[k2];
             }
+            }
             PROF_T(2);
             lds_sync();
             PROF_T(3);
@@ -372,6 +409,43 @@ __global__ void __launch_bounds__(THREADS, 1)
         lds_sync();
         PROF_T(6);
         PRIO(3);
+        if constexpr (PBS) {
+            if (fjob) {  // pass B^-1 (row kappa = u): DFT4 over i, transpose, fused DFT4
+                cplx v[4];
+#pragma unroll
+                for (int i = 0; i < 4; i++) v[i] = jbuf[baseB + SG1[i]];
+                dft4<true>(v[0], v[1], v[2], v[3]);
+                br512::transpose4(v);
+                lf512::dft4<true>(v, lf512::k4(s_lf, lf512::IB2 + 4 * r));
+#pragma unroll
+                for (int k2 = 0; k2 < 4; k2++) jbuf[baseB + SG1[k2]] = v[k2];
+            }
+            wave_sync();
+            PROF_T(7);
+            PRIO(3);
+            if (fjob) {  // pass A^-1 (column u): fused DFT4, transpose, fused DFT4, untwist, from_torus, ACC +=
+                cplx v[4];
+#pragma unroll
+                for (int i = 0; i < 4; i++) v[i] = jbuf[baseA + SG3[i]];
+                lf512::dft4<true>(v, lf512::k4(s_lf, lf512::IA1 + 4 * u));
+                br512::transpose4(v);
+                lf512::dft4<true>(v, lf512::k4(s_lf, lf512::IA2 + 4 * (4 * u + r)));
+                uint64_t *poly = acc + jb * ACC_STRIDE;
+#pragma unroll
+                for (int k2 = 0; k2 < 4; k2++) {
+                    const int j = ll + 64 * k2;  // m = r + 4 k2 -> j = u + 16 m
+                    const cplx t = cmul(v[k2], s_untw[j]);  // x 2^-8 (exact) in the conversion
+                    bool o0, o1;
+                    uint64_t a0 = torus_add_fast_sh<8>(t.re, poly[j], o0), a1 = torus_add_fast_sh<8>(t.im, poly[j + M], o1);
+                    if (__builtin_amdgcn_ballot_w64(!(o0 && o1))) {  // zeros, out-of-range magnitudes (rare)
+                        a0 = poly[j] + from_torus_bits(t.re * 0x1p-8);
+                        a1 = poly[j + M] + from_torus_bits(t.im * 0x1p-8);
+                    }
+                    poly[j] = a0;
+                    poly[j + M] = a1;
+                }
+            }
+        } else {
         cplx w16[3];  // for both inverse passes
 #pragma unroll
         for (int k = 0; k < 3; k++) w16[k] = my_w16[k];
@@ -408,6 +482,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                 poly[j] = a0;
                 poly[j + M] = a1;
             }
+        }
         }
         wave_sync();  // the next step's decomposition reads this wave's ACC writes (in-order LDS)
         PROF_T(8);

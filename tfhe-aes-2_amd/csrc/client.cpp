@@ -294,6 +294,47 @@ void sincos_2pi(long num, long den, double &c, double &s) {
 }
 }  // namespace
 
+// The blind rotation's fused-twiddle transform constants (lf512.hpp layout; the oracle's or_lf_plan_build
+// computes the same values with the same sincos): per fused stage (cos, tan) of g^2 and of g, g = e^{2 pi i
+// num / 1024}
+std::vector<double> make_lf512_table() {
+    std::vector<double> t(1700, 0.0);
+    auto ct = [&](long num, double *o) {
+        double c, s;
+        sincos_2pi(num, 1024, c, s);
+        o[0] = c;
+        o[1] = s / c;
+    };
+    auto k4 = [&](int off, long num) {
+        ct(2 * num, &t[off]);
+        ct(num, &t[off + 2]);
+    };
+    for (int k = 0; k < 4; k++) {
+        k4(0 + 4 * k, 16 - 64 * k);    // FA2
+        k4(336 + 4 * k, 1 + 64 * k);   // IB2
+    }
+    for (int a = 0; a < 16; a++) {
+        k4(16 + 4 * a, 4 - 16 * a);    // FB1
+        k4(352 + 4 * a, 4 + 16 * a);   // IA1
+        for (int l = 0; l < 4; l++) {
+            k4(80 + 4 * (4 * a + l), 1 - 4 * a - 64 * l);   // FB2
+            k4(416 + 4 * (4 * a + l), 1 + 4 * a + 64 * l);  // IA2
+        }
+    }
+    t[672] = 1.0 / std::sqrt(2.0);
+    ct(64, &t[673]);
+    for (int j = 0; j < 256; j++) {
+        double c, s;
+        sincos_2pi(j, 1024, c, s);
+        t[676 + 2 * j] = c;
+        t[676 + 2 * j + 1] = -s;
+        sincos_2pi(-((j >> 4) + (j & 3)), 1024, c, s);
+        t[1188 + 2 * j] = c;
+        t[1188 + 2 * j + 1] = s;
+    }
+    return t;
+}
+
 FftTables make_fft_tables(int N) {
     FftTables t;
     t.N = N;

@@ -125,5 +125,6 @@ struct FftTables {
     std::vector<double> twist, untwist, w;  // interleaved (re, im), M entries each
 };
 FftTables make_fft_tables(int N);
+std::vector<double> make_lf512_table();  // lf512.hpp layout
 
 }  // namespace tae

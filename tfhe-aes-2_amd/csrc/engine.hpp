@@ -229,6 +229,7 @@ class Engine {
     bool x4_512_ = false;     // N = 512, k = 4 (lvl_64): batched blind rotations br512x4 / br512lat
     long lat_max_ = 256;      // batch size up to which br512lat runs (TAE_BR_LAT_MAX)
     int num_cu_ = 256;
+    double *d_lf_ = nullptr;  // the fused-twiddle transform's table (lf512.hpp), params_sqrd_lvl_64
     bool timing_ = false, clock_ = false;
     uint64_t *d_clk_ = nullptr;
     size_t cap_clk_ = 0;

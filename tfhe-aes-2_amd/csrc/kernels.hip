@@ -620,6 +620,16 @@ __global__ void s1_gather_kernel(const uint64_t *__restrict__ in, uint64_t *__re
     }
 }
 
+// the Fourier BSK the fused-twiddle transform multiplies with (lf512.hpp): G * conj(E2(pos)) per
+// position, the oracle's lf_rescale (same cmul)
+__global__ void __launch_bounds__(kThreads) lf_rescale_kernel(cplx *__restrict__ g, size_t polys,
+                                                              const double *__restrict__ lf) {
+    const cplx *e2 = reinterpret_cast<const cplx *>(lf + lf512::E2);
+    const size_t total = polys * 256;
+    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x)
+        g[t] = cmul(g[t], e2[t & 255]);
+}
+
 unsigned grid_for(size_t total) { return (unsigned)std::min<size_t>((total + kThreads - 1) / kThreads, 65536); }
 
 constexpr int kBrC = 3;  // ciphertexts per workgroup in the batched N=512 blind rotation
@@ -736,6 +746,11 @@ void Engine::init_common() {
     // small ones.  TAE_BR_LAT_MAX (a tuning knob, both sides pinned by tests) is the batch size up
     // to which br512lat runs (0: never).
     x4_512_ = p_.N == 512 && p_.k == 4 && p_.pbs_l == 3 && p_.pbs_b == 12 && p_.cbs_l == 1 && p_.cbs_b == 13;
+    if (x4_512_) {  // the blind rotations' fused-twiddle transform (lf512.hpp)
+        const std::vector<double> lf = make_lf512_table();
+        d_lf_ = static_cast<double *>(alloc(lf.size() * 8));
+        HIPC(hipMemcpy(d_lf_, lf.data(), lf.size() * 8, hipMemcpyHostToDevice));
+    }
     const char *blat = getenv("TAE_BR_LAT_MAX");
     lat_max_ = blat ? atol(blat) : 256;
     HIPC(hipDeviceGetAttribute(&num_cu_, hipDeviceAttributeMultiprocessorCount, device_));
@@ -811,6 +826,10 @@ void Engine::bsk_to_fourier(const uint64_t *d_bsk_std) {
             d_bsk_std, d_bsk_f_, polys, d_twist_, d_w_);
     }
     HIPC(hipGetLastError());
+    if (x4_512_) {  // the blind rotations run the fused-twiddle transform: its BSK carries conj(E2)
+        lf_rescale_kernel<<<grid_for(polys * 256), kThreads, 0, stream_>>>(d_bsk_f_, polys, d_lf_);
+        HIPC(hipGetLastError());
+    }
     HIPC(hipStreamSynchronize(stream_));
 }
 
@@ -928,7 +947,7 @@ Engine::~Engine() {
                     (void *)d_ggsw_f_, (void *)d_state_, (void *)d_muls_, (void *)d_pf_bt_, (void *)d_ks_bt_, (void *)d_pf_corr_, (void *)d_pf_bt_kl_,
                     (void *)d_digits_, (void *)d_wlut_sbox_, (void *)d_wlut_id_, (void *)d_lut_x_, (void *)d_xbuf_,
                     (void *)d_xsh_, (void *)d_xks_, (void *)d_xpbs_, (void *)d_ints_, (void *)d_s1_sbox_tv_,
-                    (void *)d_s1_id_tv_, (void *)d_s1_in_, (void *)d_s1_out_, (void *)d_s1_pks_, (void *)d_s1_tv_, (void *)d_pf_flags_, (void *)d_clk_})
+                    (void *)d_s1_id_tv_, (void *)d_s1_in_, (void *)d_s1_out_, (void *)d_s1_pks_, (void *)d_s1_tv_, (void *)d_pf_flags_, (void *)d_clk_, (void *)d_lf_})
         if (q) hipFree(q);
     for (auto &e : ev_pool_) hipEventDestroy(e);
     if (caller_ev_) hipEventDestroy(caller_ev_);
@@ -985,7 +1004,7 @@ void Engine::bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint
     if (x4_512_) {
         if ((long)B <= lat_max_) {
             br512lat::br_kernel<3, 12><<<(unsigned)B, br512lat::THREADS, br512lat::lds_bytes(3), stream_>>>(
-                d_small, p_.n, d_lut_glwe, d_bsk_f_, d_big, (long)B, body_add, out_add, d_twist_, d_w_);
+                d_small, p_.n, d_lut_glwe, d_bsk_f_, d_big, (long)B, body_add, out_add, d_lf_);
             HIPC(hipGetLastError());
             return;
         }
@@ -998,7 +1017,7 @@ void Engine::bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint
         uint64_t *clk = clock_buffer(wgs);
         timed(ST_PBS_MAIN, [&] {
             br512x4::br_kernel<3, true, 12><<<wgs, br512x4::THREADS, br512x4::lds_bytes(), stream_>>>(
-                d_small, p_.n, d_lut_glwe, 0, d_bsk_f_, 0, d_big, bx, body_add, out_add, d_twist_, d_w_, clk);
+                d_small, p_.n, d_lut_glwe, 0, d_bsk_f_, 0, d_big, bx, body_add, out_add, d_twist_, d_w_, d_lf_, clk);
             HIPC(hipGetLastError());
         });
         record_clock(clk, wgs);
@@ -1006,7 +1025,7 @@ void Engine::bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint
         if (bx < (long)B) {
             br512lat::br_kernel<3, 12><<<(unsigned)(B - bx), br512lat::THREADS, br512lat::lds_bytes(3), stream_>>>(
                 d_small + (size_t)bx * (p_.n + 1), p_.n, d_lut_glwe, d_bsk_f_, d_big + (size_t)bx * p_.big_len(),
-                (long)B - bx, body_add, out_add, d_twist_, d_w_);
+                (long)B - bx, body_add, out_add, d_lf_);
             HIPC(hipGetLastError());
         }
         return;
@@ -1183,7 +1202,7 @@ void Engine::vertical_packing(const cplx *d_ggsw_f, size_t G, int n_in, const ui
     if (x4_512_) {
         const size_t wgs = G * (size_t)((n_out + kBrC - 1) / kBrC);
         br512x4::br_kernel<1, false, 13><<<(unsigned)wgs, br512x4::THREADS, br512x4::lds_bytes(), stream_>>>(
-            nullptr, 0, d_lut, n_out, d_ggsw_f, n_in, d_out, (long)G, 0, 0, d_twist_, d_w_, nullptr);
+            nullptr, 0, d_lut, n_out, d_ggsw_f, n_in, d_out, (long)G, 0, 0, d_twist_, d_w_, nullptr, nullptr);
         HIPC(hipGetLastError());
         return;
     }
