@@ -477,38 +477,43 @@ class FFT:
 
 
 class LfTransform:
-    """The blind rotation's fused-twiddle transform for N = 512 (tfhe_oracle.c or_lf_*): forward of an
-    integer digit polynomial, backward (torus add) of a spectrum that carries the factor E2, and E2's
-    conjugate (the Fourier BSK rescale)."""
+    """The blind rotation's fused-twiddle transform for N = 512 or 1024 (tfhe_oracle.c or_lf_* /
+    or_lf1k_*): forward of an integer digit polynomial, backward (torus add) of a spectrum that carries
+    the factor E2, and E2's conjugate (the Fourier BSK rescale)."""
 
-    def __init__(self):
+    def __init__(self, N: int = 512):
+        assert N in (512, 1024)
         L = lib()
-        L.or_lf_plan_new.restype = C.c_void_p
-        L.or_lf_plan_free.argtypes = [C.c_void_p]
-        L.or_lf_fwd.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.c_void_p]
-        L.or_lf_bwd_add.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64)]
-        L.or_lf_e2.argtypes = [C.c_void_p, C.c_void_p]
-        self.h = L.or_lf_plan_new()
+        self.N, self.M = N, N // 2
+        pre = "or_lf_" if N == 512 else "or_lf1k_"
+        new = getattr(L, "or_lf_plan_new" if N == 512 else "or_lf1k_plan_new")
+        new.restype = C.c_void_p
+        L.or_lf_any_free.argtypes = [C.c_void_p]
+        self._fwd, self._bwd, self._e2 = (getattr(L, pre + n) for n in ("fwd", "bwd_add", "e2"))
+        self._fwd.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.c_void_p]
+        self._bwd.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64)]
+        self._e2.argtypes = [C.c_void_p, C.c_void_p]
+        self.h = new()
 
     def __del__(self):
         try:
-            lib().or_lf_plan_free(self.h)
+            lib().or_lf_any_free(self.h)
         except Exception:
             pass
 
     def fwd_int(self, poly: np.ndarray) -> np.ndarray:
-        out = np.zeros(256, dtype=np.complex128)
-        lib().or_lf_fwd(self.h, _pi64(np.ascontiguousarray(poly, dtype=np.int64)), out.ctypes.data_as(C.c_void_p))
+        out = np.zeros(self.M, dtype=np.complex128)
+        self._fwd(self.h, _pi64(np.ascontiguousarray(poly, dtype=np.int64)), out.ctypes.data_as(C.c_void_p))
         return out
 
     def add_bwd_torus(self, four: np.ndarray, out: np.ndarray) -> np.ndarray:
         four = np.ascontiguousarray(four, dtype=np.complex128)
-        lib().or_lf_bwd_add(self.h, four.ctypes.data_as(C.c_void_p), _p64(out))
+        self._bwd(self.h, four.ctypes.data_as(C.c_void_p), _p64(out))
         return out
 
     def conj_e2(self) -> np.ndarray:
-        out = np.zeros(256, dtype=np.complex128)
-        lib().or_lf_e2(self.h, out.ctypes.data_as(C.c_void_p))
+        out = np.zeros(self.M, dtype=np.complex128)
+        self._e2(self.h, out.ctypes.data_as(C.c_void_p))
         return out
 
 

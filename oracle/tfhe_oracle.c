@@ -476,6 +476,7 @@ typedef struct {
     double c2, t2, c1, t1; /* (cos, tan) of g^2 and of g */
 } lf4;
 typedef struct {
+    int N;        /* 512 (the plans share this tag: ext_product_add dispatches on it) */
     lf4 fa2[4];   /* forward pass A, stage 2, lane row k1: g = psi^16 W16^k1          (num 16 - 64 k1) */
     lf4 fb1[16];  /* forward pass B, stage 1, lane column kappa: g = psi^4 W_M^4kappa (num 4 - 16 kappa) */
     lf4 fb2[64];  /* forward pass B, stage 2, lane (kappa, l1): g = psi W_M^kappa W16^l1 */
@@ -498,6 +499,7 @@ static void lf_make(long num, lf4 *o) {
 }
 
 static void or_lf_plan_build(lf_plan *P) {
+    P->N = 512;
     for (int k = 0; k < 4; k++) {
         lf_make(16 - 64 * k, &P->fa2[k]);
         lf_make(1 + 64 * k, &P->ib2[k]);
@@ -541,6 +543,21 @@ static void lf_dft4(const or_c64 *x, const lf4 *K, int inv, or_c64 *y) {
     y[3] = (or_c64){fma(-c, q.im, u1.re), fma(c, q.re, u1.im)};
 }
 
+/* DFT4 over i of the integer pairs d_i = d[i][0] + i d[i][1] times (e^{i pi/8})^i: the e^{i pi/4} products of
+ * the first stage act on the integers exactly ((re - im, re + im) / sqrt 2), the second stage is fused */
+static void lf_int_dft4(const int64_t d[4][2], double s2, double c8, double t8, or_c64 *q) {
+    double d0r = (double)d[0][0], d0i = (double)d[0][1], d1r = (double)d[1][0], d1i = (double)d[1][1];
+    double p2r = (double)(d[2][0] - d[2][1]), p2i = (double)(d[2][0] + d[2][1]);
+    double p3r = (double)(d[3][0] - d[3][1]), p3i = (double)(d[3][0] + d[3][1]);
+    or_c64 Ep = {fma(s2, p2r, d0r), fma(s2, p2i, d0i)}, Em = {fma(-s2, p2r, d0r), fma(-s2, p2i, d0i)};
+    or_c64 Op = {fma(s2, p3r, d1r), fma(s2, p3i, d1i)}, Om = {fma(-s2, p3r, d1r), fma(-s2, p3i, d1i)};
+    or_c64 a = lf_rot(Op, t8), b = lf_rot(Om, t8);
+    q[0] = lf_add(Ep, c8, a);
+    q[2] = lf_add(Ep, -c8, a);
+    q[1] = (or_c64){fma(c8, b.im, Em.re), fma(-c8, b.re, Em.im)};
+    q[3] = (or_c64){fma(-c8, b.im, Em.re), fma(c8, b.re, Em.im)};
+}
+
 /* forward transform of one digit polynomial (N = 512 integers) into X[16 kappa + lambda] */
 void or_lf_fwd(const void *plan, const int64_t *poly, or_c64 *X) {
     const lf_plan *P = (const lf_plan *)plan;
@@ -548,23 +565,13 @@ void or_lf_fwd(const void *plan, const int64_t *poly, or_c64 *X) {
     or_c64 z[256];
     for (int u = 0; u < 16; u++)
         for (int r = 0; r < 4; r++) {
-            double d0r, d0i, d1r, d1i, p2r, p2i, p3r, p3i;
             int64_t d[4][2];
             for (int i = 0; i < 4; i++) {
                 int j = u + 16 * r + 64 * i;
                 d[i][0] = poly[j];
                 d[i][1] = poly[j + 256];
             }
-            d0r = (double)d[0][0], d0i = (double)d[0][1], d1r = (double)d[1][0], d1i = (double)d[1][1];
-            p2r = (double)(d[2][0] - d[2][1]), p2i = (double)(d[2][0] + d[2][1]);
-            p3r = (double)(d[3][0] - d[3][1]), p3i = (double)(d[3][0] + d[3][1]);
-            or_c64 Ep = {fma(P->s2, p2r, d0r), fma(P->s2, p2i, d0i)}, Em = {fma(-P->s2, p2r, d0r), fma(-P->s2, p2i, d0i)};
-            or_c64 Op = {fma(P->s2, p3r, d1r), fma(P->s2, p3i, d1i)}, Om = {fma(-P->s2, p3r, d1r), fma(-P->s2, p3i, d1i)};
-            or_c64 a = lf_rot(Op, P->t8), b = lf_rot(Om, P->t8);
-            Q[u][r][0] = lf_add(Ep, P->c8, a);
-            Q[u][r][2] = lf_add(Ep, -P->c8, a);
-            Q[u][r][1] = (or_c64){fma(P->c8, b.im, Em.re), fma(-P->c8, b.re, Em.im)};
-            Q[u][r][3] = (or_c64){fma(-P->c8, b.im, Em.re), fma(P->c8, b.re, Em.im)};
+            lf_int_dft4(d, P->s2, P->c8, P->t8, Q[u][r]);
         }
     for (int u = 0; u < 16; u++)
         for (int k1 = 0; k1 < 4; k1++) {
@@ -638,10 +645,174 @@ void *or_lf_plan_new(void) {
 void or_lf_plan_free(void *plan) { free(plan); }
 void or_lf_e2(const void *plan, or_c64 *e2) { memcpy(e2, ((const lf_plan *)plan)->e2, sizeof(or_c64) * 256); }
 
+/* ======================================================================================
+ * The same for N = 1024 (the 8-bit model's PBS: k = 2, 6 levels of 2^7; the product's br1024 /
+ * br1024lat PBS mode).  M = 512 in or_fft_raw_fwd's three radix-8 passes (pass 0 on
+ * points t + 64 m, pass 1 on 64 gg + uu + 8 m for lane t = 8 gg + uu, pass 2 on 8 t + m; positions are
+ * its output order), every DFT8 split 2 x 4 with the twiddles fused the same way:
+ *  - DFT8 of x_m g^m relative to x_0's factor (lf_dft8): fused DFT4s of ratio g^2 over the even and the
+ *    odd m, then four fused butterflies a +- rho b, rho = g W8^k1: 72 fma instead of a DFT8 (56 flops)
+ *    plus 7 twiddle products (28);
+ *  - pass 0's inputs carry the twist psi^(t + 64 m) = psi^t (psi^64)^m: its DFT4s are the N = 512
+ *    transform's integer DFT4 (ratio psi^128 = e^{i pi/8}) and its butterflies lane-uniform; psi^t and
+ *    the twiddles W^{t kk} become pass 1's ratios g = psi^8 W^{8 gg}, the rest pass 2's ratios
+ *    g = psi W^{gg + 8 kk} (lane (gg, kk) = (t >> 3, t & 7)); the forward output is the exact DFT;
+ *  - the inverse input carries E2(pos) = psi^((pos >> 6) + ((pos >> 3) & 7)) (the Fourier BSK holds
+ *    G conj(E2)), constant over each pass-2 DFT8, which stays a plain inverse DFT8 (dftR); inverse passes
+ *    1 and 0 are fused with ratios psi W^{-8 uu} and psi W^{-t}; every ratio is off the axes.
+ * Angles 2 pi num / 2048: psi = e^{i pi / 1024} is num 1, W = W_512 num -4, W8 num -256.
+ * ====================================================================================== */
+typedef struct {
+    int N;       /* 1024 */
+    or_fft *f;   /* the plain inverse DFT8's W8 factors */
+    double s2, c8, t8; /* 1/sqrt(2); cos, tan of pi/8 (psi^128) */
+    double p0[8];      /* pass-0 butterflies: (cos, tan) of psi^64 W8^k1         (num 64 - 256 k1) */
+    double f1[8][12];  /* forward pass 1, lane group gg: g = psi^8 W^(8 gg)      (num 8 - 32 gg) */
+    double f2[64][12]; /* forward pass 2, lane t: g = psi W^((t >> 3) + 8 (t & 7)) (num 1 - 4 (t >> 3) - 32 (t & 7)) */
+    double i1[8][12];  /* inverse pass 1, lane column uu: g = psi W^(-8 uu)     (num 1 + 32 uu) */
+    double i0[64][12]; /* inverse pass 0, lane t: g = psi W^(-t)                (num 1 + 4 t) */
+    or_c64 untw[512];  /* conj(twist[j]); the backward 2^-9 is exact and applied to the sum */
+    or_c64 e2[512];    /* conj(E2(pos)) */
+} lf1k_plan;
+
+static void lf1k_ct(long num, double *c, double *t) {
+    double s;
+    sincos2pi(num, 2048, c, &s);
+    *t = s / *c;
+}
+/* a fused DFT8 of ratio g = e^{2 pi i num / 2048}: (cos, tan) of g^4, g^2 (its DFT4s), then of g W8^-+k1 */
+static void lf8_make(long num, int inv, double *e) {
+    lf1k_ct(4 * num, &e[0], &e[1]);
+    lf1k_ct(2 * num, &e[2], &e[3]);
+    for (int k1 = 0; k1 < 4; k1++) lf1k_ct(num + (inv ? 256 : -256) * k1, &e[4 + 2 * k1], &e[5 + 2 * k1]);
+}
+
+static void or_lf1k_plan_build(lf1k_plan *P) {
+    P->N = 1024;
+    P->f = or_fft_new(1024);
+    P->s2 = 1.0 / sqrt(2.0);
+    lf1k_ct(128, &P->c8, &P->t8);
+    for (int k1 = 0; k1 < 4; k1++) lf1k_ct(64 - 256 * k1, &P->p0[2 * k1], &P->p0[2 * k1 + 1]);
+    for (int g = 0; g < 8; g++) {
+        lf8_make(8 - 32 * g, 0, P->f1[g]);
+        lf8_make(1 + 32 * g, 1, P->i1[g]);
+    }
+    for (int t = 0; t < 64; t++) {
+        lf8_make(1 - 4 * (t >> 3) - 32 * (t & 7), 0, P->f2[t]);
+        lf8_make(1 + 4 * t, 1, P->i0[t]);
+    }
+    for (int j = 0; j < 512; j++) {
+        double c, s;
+        sincos2pi(j, 2048, &c, &s);
+        P->untw[j].re = c;
+        P->untw[j].im = -s;
+        sincos2pi(-((j >> 6) + ((j >> 3) & 7)), 2048, &c, &s);
+        P->e2[j].re = c;
+        P->e2[j].im = s;
+    }
+}
+
+/* DFT8 (W8 forward / conj inverse) of x_m g^m relative to x_0's factor, natural order out */
+static void lf_dft8(const or_c64 *x, const double *e, int inv, or_c64 *y) {
+    const lf4 K = {e[0], e[1], e[2], e[3]};
+    or_c64 a[4] = {x[0], x[2], x[4], x[6]}, b[4] = {x[1], x[3], x[5], x[7]}, A[4], B[4];
+    lf_dft4(a, &K, inv, A);
+    lf_dft4(b, &K, inv, B);
+    for (int k1 = 0; k1 < 4; k1++) {
+        or_c64 r = lf_rot(B[k1], e[5 + 2 * k1]);
+        y[k1] = lf_add(A[k1], e[4 + 2 * k1], r);
+        y[k1 + 4] = lf_add(A[k1], -e[4 + 2 * k1], r);
+    }
+}
+
+/* forward transform of one digit polynomial (N = 1024 integers) into X[pos] */
+void or_lf1k_fwd(const void *plan, const int64_t *poly, or_c64 *X) {
+    const lf1k_plan *P = (const lf1k_plan *)plan;
+    or_c64 z[512], z2[512];
+    for (int t = 0; t < 64; t++) {
+        or_c64 A[2][4];
+        for (int n1 = 0; n1 < 2; n1++) {
+            int64_t d[4][2];
+            for (int i = 0; i < 4; i++) {
+                int j = t + 64 * (n1 + 2 * i);
+                d[i][0] = poly[j];
+                d[i][1] = poly[j + 512];
+            }
+            lf_int_dft4(d, P->s2, P->c8, P->t8, A[n1]);
+        }
+        for (int k1 = 0; k1 < 4; k1++) {
+            or_c64 r = lf_rot(A[1][k1], P->p0[2 * k1 + 1]);
+            z[t + 64 * k1] = lf_add(A[0][k1], P->p0[2 * k1], r);
+            z[t + 64 * (k1 + 4)] = lf_add(A[0][k1], -P->p0[2 * k1], r);
+        }
+    }
+    for (int t = 0; t < 64; t++) {
+        int gg = t >> 3, uu = t & 7;
+        or_c64 x[8], y[8];
+        for (int m = 0; m < 8; m++) x[m] = z[64 * gg + uu + 8 * m];
+        lf_dft8(x, P->f1[gg], 0, y);
+        for (int k = 0; k < 8; k++) z2[64 * gg + uu + 8 * k] = y[k];
+    }
+    for (int t = 0; t < 64; t++) {
+        or_c64 x[8], y[8];
+        for (int m = 0; m < 8; m++) x[m] = z2[8 * t + m];
+        lf_dft8(x, P->f2[t], 0, y);
+        for (int k = 0; k < 8; k++) X[8 * t + k] = y[k];
+    }
+}
+
+/* backward transform of Y[pos] (which carries the factor E2) added to the torus polynomial out
+ * (N = 1024): untwist conj(twist), 2^-9 exact, from_torus */
+void or_lf1k_bwd_add(const void *plan, const or_c64 *Y, uint64_t *out) {
+    const lf1k_plan *P = (const lf1k_plan *)plan;
+    or_c64 z[512], z2[512];
+    for (int t = 0; t < 64; t++) {
+        or_c64 v[8];
+        for (int k = 0; k < 8; k++) v[k] = Y[8 * t + k];
+        dftR(P->f, v, 8, 1);
+        for (int m = 0; m < 8; m++) z[8 * t + m] = v[m];
+    }
+    for (int t = 0; t < 64; t++) {
+        int gg = t >> 3, uu = t & 7;
+        or_c64 x[8], y[8];
+        for (int k = 0; k < 8; k++) x[k] = z[64 * gg + uu + 8 * k];
+        lf_dft8(x, P->i1[uu], 1, y);
+        for (int m = 0; m < 8; m++) z2[64 * gg + uu + 8 * m] = y[m];
+    }
+    for (int t = 0; t < 64; t++) {
+        or_c64 x[8], y[8];
+        for (int k = 0; k < 8; k++) x[k] = z2[t + 64 * k];
+        lf_dft8(x, P->i0[t], 1, y);
+        for (int m = 0; m < 8; m++) {
+            int j = t + 64 * m;
+            or_c64 tt = cmul(y[m], P->untw[j]);
+            out[j] += or_from_torus(tt.re * 0x1p-9);
+            out[j + 512] += or_from_torus(tt.im * 0x1p-9);
+        }
+    }
+}
+
+void *or_lf1k_plan_new(void) {
+    lf1k_plan *P = (lf1k_plan *)malloc(sizeof(lf1k_plan));
+    or_lf1k_plan_build(P);
+    return P;
+}
+void or_lf1k_e2(const void *plan, or_c64 *e2) { memcpy(e2, ((const lf1k_plan *)plan)->e2, sizeof(or_c64) * 512); }
+
+/* either plan (the tag is its first member) */
+static int lf_plan_n(const void *plan) { return *(const int *)plan; }
+void or_lf_any_free(void *plan) {
+    if (!plan) return;
+    if (lf_plan_n(plan) == 1024) or_fft_free(((lf1k_plan *)plan)->f);
+    free(plan);
+}
+
 /* the Fourier BSK the fused transform multiplies with: G * conj(E2(pos)) per position */
-static void lf_rescale(const lf_plan *P, or_c64 *G, size_t polys) {
+static void lf_rescale(const void *plan, or_c64 *G, size_t polys) {
+    const int M = lf_plan_n(plan) / 2;
+    const or_c64 *e2 = M == 256 ? ((const lf_plan *)plan)->e2 : ((const lf1k_plan *)plan)->e2;
     for (size_t i = 0; i < polys; i++)
-        for (int f = 0; f < 256; f++) G[i * 256 + f] = cmul(G[i * 256 + f], P->e2[f]);
+        for (int f = 0; f < M; f++) G[i * M + f] = cmul(G[i * M + f], e2[f]);
 }
 
 /* ======================================================================================
@@ -776,6 +947,9 @@ static void *kg_worker(void *arg) {
 /* the parameter sets whose blind rotation runs the fused-twiddle transform (the product's br512x4 /
  * br512lat shape: N = 512, k = 4, 3 levels of 2^12 = params_sqrd_lvl_64) */
 static int lf_set(const or_params *p) { return p->N == 512 && p->k == 4 && p->pbs_l == 3 && p->pbs_b == 12; }
+/* ... and the N = 1024 one (the product's br1024 / br1024lat PBS shape: k = 2, 6 levels of 2^7, the 8-bit
+ * model's set) */
+static int lf1k_set(const or_params *p) { return p->N == 1024 && p->k == 2 && p->pbs_l == 6 && p->pbs_b == 7; }
 
 static void server_key_fourier(or_server_key *sk) {
     const or_params *p = &sk->p;
@@ -785,10 +959,9 @@ static void server_key_fourier(or_server_key *sk) {
     for (size_t i = 0; i < polys; i++)
         or_fft_fwd_torus(sk->fft, sk->bsk + i * p->N, sk->bsk_f + i * M);
     sk->lf = NULL;
-    if (lf_set(p)) {
-        sk->lf = or_lf_plan_new();
-        lf_rescale((const lf_plan *)sk->lf, sk->bsk_f, polys);
-    }
+    if (lf_set(p)) sk->lf = or_lf_plan_new();
+    if (lf1k_set(p)) sk->lf = or_lf1k_plan_new();
+    if (sk->lf) lf_rescale(sk->lf, sk->bsk_f, polys);
 }
 
 /* shortint_woppbs_1bit.rs:245-268 (gen_keys + new_wopbs_key_only_for_wopbs) */
@@ -860,7 +1033,7 @@ void or_server_key_free(or_server_key *sk) {
     free(sk->pfpksk);
     free(sk->bsk_f);
     or_fft_free(sk->fft);
-    or_lf_plan_free(sk->lf);
+    or_lf_any_free(sk->lf);
     free(sk);
 }
 
@@ -955,7 +1128,9 @@ static void ext_product_add(const or_server_key *sk, const void *lf, const or_c6
     for (int lev = levels; lev >= 1; lev--) {
         for (int r = 0; r <= k; r++) {
             memcpy(poly, dig + (size_t)(lev - 1) * glwe + (size_t)r * N, sizeof(int64_t) * N);
-            if (lf)
+            if (lf && lf_plan_n(lf) == 1024)
+                or_lf1k_fwd(lf, poly, X);
+            else if (lf)
                 or_lf_fwd(lf, poly, X);
             else
                 or_fft_fwd_int(sk->fft, poly, X);
@@ -975,7 +1150,9 @@ static void ext_product_add(const or_server_key *sk, const void *lf, const or_c6
         }
     }
     for (int c = 0; c <= k; c++) {
-        if (lf)
+        if (lf && lf_plan_n(lf) == 1024)
+            or_lf1k_bwd_add(lf, acc + (size_t)c * M, out + (size_t)c * N);
+        else if (lf)
             or_lf_bwd_add(lf, acc + (size_t)c * M, out + (size_t)c * N);
         else
             or_fft_add_bwd_torus(sk->fft, acc + (size_t)c * M, out + (size_t)c * N);

@@ -91,6 +91,12 @@ void or_lf_plan_free(void *plan);
 void or_lf_fwd(const void *plan, const int64_t *poly, or_c64 *X);
 void or_lf_bwd_add(const void *plan, const or_c64 *Y, uint64_t *out);
 void or_lf_e2(const void *plan, or_c64 *e2 /*[256]*/);
+/* ... and for N = 1024 (the 8-bit model's PBS); or_lf_any_free frees either plan */
+void *or_lf1k_plan_new(void);
+void or_lf1k_fwd(const void *plan, const int64_t *poly, or_c64 *X);
+void or_lf1k_bwd_add(const void *plan, const or_c64 *Y, uint64_t *out);
+void or_lf1k_e2(const void *plan, or_c64 *e2 /*[512]*/);
+void or_lf_any_free(void *plan);
 void or_fft_raw_fwd(const or_fft *f, or_c64 *z);
 void or_fft_raw_inv(const or_fft *f, or_c64 *z);
 
@@ -108,8 +114,9 @@ typedef struct {
     uint64_t *pfpksk; /* [k+1][K+1][pfks_l][(k+1)*N] */
     or_c64 *bsk_f;    /* [n][pbs_l][k+1][k+1][N/2] Fourier domain */
     or_fft *fft;
-    void *lf;         /* params_sqrd_lvl_64: the blind rotation's fused-twiddle transform (lf_plan), and
-                         bsk_f holds the BSK spectrum times conj(E2); NULL otherwise */
+    void *lf;         /* params_sqrd_lvl_64 and the 8-bit model's set: the blind rotation's fused-twiddle
+                         transform (lf_plan / lf1k_plan), and bsk_f holds the BSK spectrum times conj(E2);
+                         NULL otherwise */
 } or_server_key;
 
 int or_gen_keys(int param_id, const uint8_t seed[32], int threads, or_client_key **ck,

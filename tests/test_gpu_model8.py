@@ -58,19 +58,19 @@ def test_pbs_shift_boolean8_bit_exact(gpu_context8, oracle_keys8, client8, level
         assert min(err, (1 << 64) - err) < 1 << (63 - 6 * level), (i, level)  # within alpha
 
 
-@pytest.mark.parametrize("lat,pair,stream,B", [("1", "1", "1", 5), ("0", "1", "1", 5), ("0", "0", "1", 5),
-                                               ("1", "1", "1", 300), ("1", "1", "0", 300), ("1", "1", "1", 513)])
-def test_pbs8_kernel_variants_bit_exact(product_raw8, oracle_keys8, client8, lat, pair, stream, B):
-    """The N=1024 blind-rotation variants the engine picks: for batches up to one ciphertext per CU
-    the 1024-thread latency kernel (br1024lat, default), or with TAE_B1K_LAT=0 br1024 with one
-    ciphertext per workgroup and two levels per pass (or one: TAE_B1K_PAIR=0); and two ciphertexts
-    per workgroup (B > the CU count, odd tail workgroup of one): br1024's level-by-level kernel (default,
-    TAE_B1K_STREAM=0) or br1024s with the FFT jobs streamed across the levels (TAE_B1K_STREAM=1)."""
-    os.environ["TAE_B1K_LAT"], os.environ["TAE_B1K_PAIR"], os.environ["TAE_B1K_STREAM"] = lat, pair, stream
+@pytest.mark.parametrize("lat,pair,B", [("1", "1", 5), ("0", "1", 5), ("0", "0", 5), ("1", "1", 300),
+                                        ("1", "1", 513)])
+def test_pbs8_kernel_variants_bit_exact(product_raw8, oracle_keys8, client8, lat, pair, B):
+    """The N=1024 blind-rotation variants the engine picks, all on the fused-twiddle transform (lf1k.hpp,
+    the oracle's or_lf1k_*): for batches up to one ciphertext per CU the 1024-thread latency kernel
+    (br1024lat, default), or with TAE_B1K_LAT=0 br1024 with one ciphertext per workgroup and two levels
+    per pass (or one: TAE_B1K_PAIR=0); and two ciphertexts per workgroup (B > the CU count, odd tail
+    workgroup of one)."""
+    os.environ["TAE_B1K_LAT"], os.environ["TAE_B1K_PAIR"] = lat, pair
     try:
         ctx = tfhe_aes.context_from_raw(tfhe_aes.PARAMS_WOPPBS_8BIT, product_raw8[1], device=0)
     finally:
-        del os.environ["TAE_B1K_LAT"], os.environ["TAE_B1K_PAIR"], os.environ["TAE_B1K_STREAM"]
+        del os.environ["TAE_B1K_LAT"], os.environ["TAE_B1K_PAIR"]
     bits = np.random.default_rng(B).integers(0, 2, size=B).astype(np.uint8)
     small = client8.encrypt_bits_raw(bits, start_index=900)
     out = np.zeros((B, BIG), dtype=np.uint64)

@@ -101,6 +101,50 @@ def test_lf_negacyclic_product_within_bound(oracle_mod):
         assert e_lf < 4 * max(e_std, 1) and e_lf < 2**16
 
 
+def test_lf1k_transform_is_the_negacyclic_dft(oracle_mod):
+    """The N = 1024 fused-twiddle transform (the 8-bit model's PBS) against the radix-8
+    schedule and the definition sum (positions 64 a + 8 b + c hold frequency a + 8 b + 64 c); no output
+    factor."""
+    F, T = oracle_mod.FFT(1024), oracle_mod.LfTransform(1024)
+    rng = np.random.default_rng(13)
+    j = np.arange(512)
+    pos = np.arange(512)
+    freq = (pos >> 6) + 8 * ((pos >> 3) & 7) + 64 * (pos & 7)
+    W = np.exp(1j * np.pi * j / 1024)[None, :] * np.exp(-2j * np.pi * np.outer(freq, j) / 512)
+    for _ in range(5):
+        d = rng.integers(-64, 65, size=1024).astype(np.int64)
+        x_lf, x_std = T.fwd_int(d), F.fwd_int(d)
+        exact = W @ (d[:512] + 1j * d[512:])
+        scale = np.max(np.abs(exact))
+        assert np.max(np.abs(x_lf - x_std)) / scale < 1e-15
+        assert np.max(np.abs(x_lf - exact)) / scale < 1e-12
+
+
+def test_lf1k_negacyclic_product_within_bound(oracle_mod):
+    """The N = 1024 fused transform's external-product arithmetic against the exact negacyclic product, the
+    BSK side times conj(E2): within the radix-8 schedule's bound, and a round trip as tight as its."""
+    F, T = oracle_mod.FFT(1024), oracle_mod.LfTransform(1024)
+    e2 = T.conj_e2()
+    assert np.allclose(np.abs(e2), 1.0)
+    rng = np.random.default_rng(14)
+    for _ in range(3):
+        a = rng.integers(0, 2**64 - 1, size=1024, dtype=np.uint64)
+        b = rng.integers(-64, 65, size=1024).astype(np.int64)
+        exact = oracle_mod.negacyclic_mul_exact(a, b)
+        out, ref = np.zeros(1024, dtype=np.uint64), np.zeros(1024, dtype=np.uint64)
+        T.add_bwd_torus(F.fwd_torus(a) * e2 * T.fwd_int(b), out)
+        F.add_bwd_torus(F.fwd_torus(a) * F.fwd_int(b), ref)
+        err = np.max(np.abs((out - exact).astype(np.int64)))
+        err_std = np.max(np.abs((ref - exact).astype(np.int64)))
+        assert err < 2**32 and err < 4 * max(err_std, 1)
+        rt_lf, rt_std = np.zeros(1024, dtype=np.uint64), np.zeros(1024, dtype=np.uint64)
+        T.add_bwd_torus(F.fwd_torus(a) * e2, rt_lf)
+        F.add_bwd_torus(F.fwd_torus(a), rt_std)
+        e_lf = np.max(np.abs((rt_lf - a).astype(np.int64)))
+        e_std = np.max(np.abs((rt_std - a).astype(np.int64)))
+        assert e_lf < 4 * max(e_std, 1) and e_lf < 2**16
+
+
 def test_generate_luts_exact_layout(oracle_mod, golden):
     """shortint_woppbs_1bit.rs:665-697 (vertical packing and multi-polynomial LUT layout)."""
     lut = oracle_mod.generate_lut(16, 3, 2, lambda v: v)

@@ -15,6 +15,7 @@
 // b128 accesses at strides 1, 8 and 64), twist / W_512 / untwist tables.
 #pragma once
 #include "br512.hpp"
+#include "lf1k.hpp"
 
 namespace tae {
 namespace br1024 {
@@ -114,14 +115,18 @@ __global__ void __launch_bounds__(THREADS, 1)
     br_kernel(const uint64_t *__restrict__ lwe_in, int n, const uint64_t *__restrict__ lut, int n_out,
               const cplx *__restrict__ ggsw_base, int n_in, uint64_t *__restrict__ out, long B,
               uint64_t body_add, uint64_t out_add, const cplx *__restrict__ twist, const cplx *__restrict__ untwist,
-              const cplx *__restrict__ wtab, uint64_t *__restrict__ clk) {
+              const cplx *__restrict__ wtab, const double *__restrict__ lf, uint64_t *__restrict__ clk) {
     static_assert(LEV % LP == 0, "levels per pass must divide the level count");
+    // the 8-bit model's PBS runs the fused-twiddle transform (lf1k.hpp) on a BSK rescaled by conj(E2)
+    constexpr bool LFT = PBS && LEV == 6 && BLOG == 7;
     ClockStamp stamp;
     stamp.start(clk);
     constexpr int LOGN = 10, CJ = C * K1, JOBS = CJ * LP;
     extern __shared__ __align__(16) unsigned char smem[];
     uint64_t *acc = reinterpret_cast<uint64_t *>(smem);           // [CJ][ACC_STRIDE]
     cplx *buf = reinterpret_cast<cplx *>(acc + CJ * ACC_STRIDE);  // [JOBS][BUF_STRIDE], job = (lh, ct, p)
+    double *s_lf = reinterpret_cast<double *>(buf + JOBS * BUF_STRIDE);  // LFT: lf1k.hpp's table, else:
+    const cplx *s_untw = reinterpret_cast<const cplx *>(s_lf + lf1k::UNTW);
     cplx *s_tw = buf + JOBS * BUF_STRIDE;                           // twist
     cplx *s_w = s_tw + M;                                           // W_512 table
     cplx *s_utw = s_w + M;                                          // untwist = conj(twist) / M
@@ -151,13 +156,17 @@ __global__ void __launch_bounds__(THREADS, 1)
     }
     const bool jvalid = fjob && jct < nct;
 
-    for (int i = tid; i < M; i += THREADS) {
-        s_tw[i] = twist[i];
-        s_w[i] = wtab[i];
-        s_utw[i] = untwist[i];
+    if constexpr (LFT) {
+        for (int i = tid; i < lf1k::KERNEL_DOUBLES; i += THREADS) s_lf[i] = lf[i];
+    } else {
+        for (int i = tid; i < M; i += THREADS) {
+            s_tw[i] = twist[i];
+            s_w[i] = wtab[i];
+            s_utw[i] = untwist[i];
+        }
+        for (int i = tid; i < 7 * 64; i += THREADS) s_w0[i] = wtab[(i & 63) * ((i >> 6) + 1)];
+        if (tid < 7 * 8) s_w1[tid] = wtab[8 * (tid & 7) * ((tid >> 3) + 1)];
     }
-    for (int i = tid; i < 7 * 64; i += THREADS) s_w0[i] = wtab[(i & 63) * ((i >> 6) + 1)];
-    if (tid < 7 * 8) s_w1[tid] = wtab[8 * (tid & 7) * ((tid >> 3) + 1)];
     const cplx *gbase = PBS ? ggsw_base : ggsw_base + (size_t)g * n_in * ggsw_sz;
     const uint32_t gbytes = (uint32_t)((size_t)(PBS ? n : n_in) * ggsw_sz * sizeof(cplx));
     const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc((void *)gbase, (short)0, gbytes, 0x00020000);
@@ -181,14 +190,26 @@ __global__ void __launch_bounds__(THREADS, 1)
         acc[job * ACC_STRIDE + j] = v;
     }
     br512::lds_sync();
-    const cplx w81 = s_w[64], w83 = s_w[192];
+    const cplx w81 = LFT ? wtab[64] : s_w[64], w83 = LFT ? wtab[192] : s_w[192];
     // The lane's pass-0 / pass-1 twiddles are the same for every FFT of the launch. With LP = 1 the
     // register budget (two waves per SIMD) holds them, which saves 14 LDS reads per FFT job: the CBS
     // launch (C = 2, 2048 ciphertexts) takes 64.1 ms instead of 70.9, same box. The LP = 2 variant
     // would spill.
     constexpr bool WREG = LP == 1;
     cplx w0r[7], w1r[7];
-    if constexpr (WREG) {
+    // LFT: likewise the lane's fused-DFT8 constants of the forward passes 1 / 2 and the inverse passes
+    // 1 / 0, and the lane-uniform ones of pass 0
+    lf1k::K8 kf1, kf2, ki1, ki0;
+    lf1k::P0c k0;
+    if constexpr (LFT) {
+        k0 = lf1k::p0(lf);
+        if constexpr (WREG) {
+            kf1 = lf1k::k8(s_lf, lf1k::F1, 8, t >> 3);
+            kf2 = lf1k::k8(s_lf, lf1k::F2, 64, t);
+            ki1 = lf1k::k8(s_lf, lf1k::I1, 8, t & 7);
+            ki0 = lf1k::k8(s_lf, lf1k::I0, 64, t);
+        }
+    } else if constexpr (WREG) {
 #pragma unroll
         for (int kk = 1; kk < 8; kk++) {
             w0r[kk - 1] = s_w0[(kk - 1) * 64 + (tid & 63)];
@@ -198,7 +219,7 @@ __global__ void __launch_bounds__(THREADS, 1)
     // likewise the lane's eight twist factors of pass 0, for the 8-bit model's shapes where it was
     // measured (62.2 vs 64.1 ms for the CBS launch, same box, although its PBS instantiation then
     // spills 18 VGPRs outside the FFT passes; the lvl_1/4/256 shapes would spill more, unmeasured)
-    constexpr bool TWREG = WREG && BLOG <= 7;
+    constexpr bool TWREG = WREG && BLOG <= 7 && !LFT;
     cplx twr[8];
     if constexpr (TWREG) {
 #pragma unroll
@@ -207,6 +228,10 @@ __global__ void __launch_bounds__(THREADS, 1)
 #define TW_AT(m) (TWREG ? twr[m] : s_tw[tt + 64 * (m)])
 #define W0_AT(kk) (WREG ? w0r[(kk) - 1] : s_w0[((kk) - 1) * 64 + tt])
 #define W1_AT(kk) (WREG ? w1r[(kk) - 1] : s_w1[((kk) - 1) * 8 + uu])
+#define KF1 (WREG ? kf1 : lf1k::k8(s_lf, lf1k::F1, 8, gg))
+#define KF2 (WREG ? kf2 : lf1k::k8(s_lf, lf1k::F2, 64, tt))
+#define KI1 (WREG ? ki1 : lf1k::k8(s_lf, lf1k::I1, 8, uu))
+#define KI0 (WREG ? ki0 : lf1k::k8(s_lf, lf1k::I0, 64, tt))
 
     const int steps = PBS ? n : n_in;
     uint64_t a_next = (PBS && jvalid) ? lwe_in[(size_t)(ct0 + jct) * (n + 1)] : 0;
@@ -281,6 +306,25 @@ __global__ void __launch_bounds__(THREADS, 1)
             if (fjob) {
                 cplx *X = buf + jb * BUF_STRIDE;
                 cplx v[8];
+                if constexpr (LFT) {
+                    // fused pass 0 (lf1k::pass0) of the level's digits -> position t + 64 kk
+                    int dr[8], di[8];
+                    const int wsel = (lev - 1) >> 1, sh = ((lev - 1) & 1) * 16;
+#pragma unroll
+                    for (int m = 0; m < 8; m++) {
+                        uint32_t dw = dig[0][m];
+#pragma unroll
+                        for (int w = 1; w < DW; w++) {
+                            const uint32_t msk = 0u - (uint32_t)(wsel == w);
+                            dw = (dw & ~msk) | (dig[w][m] & msk);
+                        }
+                        dr[m] = __builtin_amdgcn_sbfe(dw, sh, 8);
+                        di[m] = __builtin_amdgcn_sbfe(dw, sh + 8, 8);
+                    }
+                    lf1k::pass0(dr, di, v, k0);
+#pragma unroll
+                    for (int kk = 0; kk < 8; kk++) X[pidx(tt + 64 * kk)] = v[kk];
+                } else {
                 // pass 0: twist, DFT8 over m, w[t kk] -> position t + 64 kk
 #pragma unroll
                 for (int m = 0; m < 8; m++) {
@@ -317,6 +361,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                     const cplx tv = cmul(v[kk], W0_AT(kk));
                     X[pidx(tt + 64 * kk)] = tv;  // W^0 = 1 exactly: only the sign of a zero can differ from skipping it
                 }
+                }
                 wave_sync();
                 if (lev0 == LEV) s_setprio_c<1>(); else s_setprio_c<2>();
                 // pass 1: points 64 gg + uu + 8 m, w[8 uu kk]
@@ -324,12 +369,18 @@ __global__ void __launch_bounds__(THREADS, 1)
                     const int gg = tt >> 3, uu = tt & 7;
 #pragma unroll
                     for (int m = 0; m < 8; m++) v[m] = X[pidx(64 * gg + uu + 8 * m)];
-                    dft8<false>(v, w81, w83);
-                    X[pidx(64 * gg + uu)] = v[0];
+                    if constexpr (LFT) {
+                        lf1k::dft8<false>(v, KF1);
 #pragma unroll
-                    for (int kk = 1; kk < 8; kk++) {
-                        const cplx tv = cmul(v[kk], W1_AT(kk));
-                        X[pidx(64 * gg + uu + 8 * kk)] = tv;  // W^0 = 1 exactly: only the sign of a zero can differ from skipping it
+                        for (int kk = 0; kk < 8; kk++) X[pidx(64 * gg + uu + 8 * kk)] = v[kk];
+                    } else {
+                        dft8<false>(v, w81, w83);
+                        X[pidx(64 * gg + uu)] = v[0];
+#pragma unroll
+                        for (int kk = 1; kk < 8; kk++) {
+                            const cplx tv = cmul(v[kk], W1_AT(kk));
+                            X[pidx(64 * gg + uu + 8 * kk)] = tv;  // W^0 = 1 exactly: only the sign of a zero can differ from skipping it
+                        }
                     }
                 }
                 wave_sync();
@@ -337,7 +388,8 @@ __global__ void __launch_bounds__(THREADS, 1)
                 // pass 2: points 8 t + m, no twiddles
 #pragma unroll
                 for (int m = 0; m < 8; m++) v[m] = X[pidx(8 * tt + m)];
-                dft8<false>(v, w81, w83);
+                if constexpr (LFT) lf1k::dft8<false>(v, KF2);
+                else dft8<false>(v, w81, w83);
 #pragma unroll
                 for (int kk = 0; kk < 8; kk++) X[pidx(8 * tt + kk)] = v[kk];
             }
@@ -392,38 +444,53 @@ __global__ void __launch_bounds__(THREADS, 1)
             // inverse pass 1: conj(w[8 uu kk]) on points 64 gg + uu + 8 kk
             {
                 const int gg = tt >> 3, uu = tt & 7;
-                v[0] = Y[pidx(64 * gg + uu)];
+                if constexpr (LFT) {
 #pragma unroll
-                for (int kk = 1; kk < 8; kk++) {
-                    const cplx y = Y[pidx(64 * gg + uu + 8 * kk)];
-                    const cplx tv = cmul(y, cconj(W1_AT(kk)));
-                    v[kk] = tv;  // W^0 = 1 exactly: only the sign of a zero can differ from skipping it
+                    for (int kk = 0; kk < 8; kk++) v[kk] = Y[pidx(64 * gg + uu + 8 * kk)];
+                    lf1k::dft8<true>(v, KI1);
+                } else {
+                    v[0] = Y[pidx(64 * gg + uu)];
+#pragma unroll
+                    for (int kk = 1; kk < 8; kk++) {
+                        const cplx y = Y[pidx(64 * gg + uu + 8 * kk)];
+                        const cplx tv = cmul(y, cconj(W1_AT(kk)));
+                        v[kk] = tv;  // W^0 = 1 exactly: only the sign of a zero can differ from skipping it
+                    }
+                    dft8<true>(v, w81, w83);
                 }
-                dft8<true>(v, w81, w83);
 #pragma unroll
                 for (int m = 0; m < 8; m++) Y[pidx(64 * gg + uu + 8 * m)] = v[m];
             }
             wave_sync();
             s_setprio_c<2>();
             // inverse pass 0: conj(w[t kk]) on points t + 64 kk, untwist, from_torus, ACC +=
-            v[0] = Y[pidx(tt)];
+            if constexpr (LFT) {
 #pragma unroll
-            for (int kk = 1; kk < 8; kk++) {
-                const cplx y = Y[pidx(tt + 64 * kk)];
-                const cplx tv = cmul(y, cconj(W0_AT(kk)));
-                v[kk] = tv;  // W^0 = 1 exactly: only the sign of a zero can differ from skipping it
+                for (int kk = 0; kk < 8; kk++) v[kk] = Y[pidx(tt + 64 * kk)];
+                lf1k::dft8<true>(v, KI0);
+            } else {
+                v[0] = Y[pidx(tt)];
+#pragma unroll
+                for (int kk = 1; kk < 8; kk++) {
+                    const cplx y = Y[pidx(tt + 64 * kk)];
+                    const cplx tv = cmul(y, cconj(W0_AT(kk)));
+                    v[kk] = tv;  // W^0 = 1 exactly: only the sign of a zero can differ from skipping it
+                }
+                dft8<true>(v, w81, w83);
             }
-            dft8<true>(v, w81, w83);
             uint64_t *poly = acc + jb * ACC_STRIDE;
 #pragma unroll
             for (int m = 0; m < 8; m++) {
                 const int j = tt + 64 * m;
-                const cplx t = cmul(v[m], s_utw[j]);
+                // untwist; LFT: by conj(twist), the 2^-9 going into the exponent (exact)
+                constexpr int SH = LFT ? 9 : 0;
+                constexpr double SC = LFT ? 0x1p-9 : 1.0;
+                const cplx t = cmul(v[m], LFT ? s_untw[j] : s_utw[j]);
                 bool o0, o1;
-                uint64_t a0 = torus_add_fast(t.re, poly[j], o0), a1 = torus_add_fast(t.im, poly[j + M], o1);
+                uint64_t a0 = torus_add_fast_sh<SH>(t.re, poly[j], o0), a1 = torus_add_fast_sh<SH>(t.im, poly[j + M], o1);
                 if (__builtin_amdgcn_ballot_w64(!(o0 && o1))) {  // zeros, out-of-range magnitudes (rare)
-                    a0 = poly[j] + from_torus_bits(t.re);
-                    a1 = poly[j + M] + from_torus_bits(t.im);
+                    a0 = poly[j] + from_torus_bits(t.re * SC);
+                    a1 = poly[j + M] + from_torus_bits(t.im * SC);
                 }
                 poly[j] = a0;
                 poly[j + M] = a1;
@@ -457,15 +524,20 @@ __global__ void __launch_bounds__(THREADS, 1)
 #undef W0_AT
 #undef W1_AT
 #undef TW_AT
+#undef KF1
+#undef KF2
+#undef KI1
+#undef KI0
 
-inline size_t lds_bytes(int C, int LP = 1) {
-    return (size_t)C * K1 * ACC_STRIDE * 8 + (size_t)C * K1 * LP * BUF_STRIDE * 16 + 3 * (size_t)M * 16 +
-           (7 * 64 + 7 * 8) * 16;
+// lft: the fused-twiddle transform's table (22 KiB) in place of br1024's twiddle tables (31 KiB)
+inline size_t lds_bytes(int C, int LP = 1, bool lft = false) {
+    return (size_t)C * K1 * ACC_STRIDE * 8 + (size_t)C * K1 * LP * BUF_STRIDE * 16 +
+           (lft ? (size_t)lf1k::KERNEL_DOUBLES * 8 : 3 * (size_t)M * 16 + (7 * 64 + 7 * 8) * 16);
 }
 
 // (levels, base_log) combinations of the N=1024 parameter sets: returns the kernel or nullptr
 typedef void (*kernel_t)(const uint64_t *, int, const uint64_t *, int, const cplx *, int, uint64_t *, long, uint64_t,
-                         uint64_t, const cplx *, const cplx *, const cplx *, uint64_t *);
+                         uint64_t, const cplx *, const cplx *, const cplx *, const double *, uint64_t *);
 // LP levels per pass; LP = 2 only for the PBS with at least two passes (nullptr otherwise)
 template <int C, int LP = 1>
 inline kernel_t pick(bool pbs, int levels, int base_log) {

@@ -11,9 +11,10 @@
 //        each chain p ascending with the oracle's fma order, the pass's levels descending
 //   S  MAC results -> LDS;  I  inverse FFT of the 3 outputs (waves 0-2);  I2 untwist, torus, ACC +=
 //      over all 16 waves
-// Every output keeps br1024's (and the oracle's) operation order: results are bit-identical to it.
-// LDS (155 KiB): ACC [3][1024] u64, spectra [3 LP][576] cplx, twist / W_512 / untwist and the pass-0/1
-// twiddle tables, digits [LEV][3][512] (int8 pairs).
+// The FFTs are br1024's fused-twiddle transform (lf1k.hpp) and every output keeps br1024's (and the
+// oracle's) operation order: results are bit-identical to it.
+// LDS (146 KiB): ACC [3][1024] u64, spectra [3 LP][576] cplx, the transform's table, digits [LEV][3][512]
+// (int8 pairs).
 #pragma once
 #include "br1024.hpp"
 
@@ -51,7 +52,7 @@ constexpr int THREADS = 1024;
 
 template <int LEV, int BLOG, int LP>
 constexpr size_t lds_bytes() {
-    return (size_t)K1 * N * 8 + (size_t)LP * K1 * BUF_STRIDE * 16 + 3 * (size_t)M * 16 + (7 * 64 + 7 * 8) * 16 +
+    return (size_t)K1 * N * 8 + (size_t)LP * K1 * BUF_STRIDE * 16 + (size_t)lf1k::KERNEL_DOUBLES * 8 +
            (size_t)LEV * K1 * M * 2;
 }
 
@@ -59,20 +60,17 @@ template <int LEV, int BLOG, int LP>
 __global__ void __launch_bounds__(THREADS, 1)
     br_kernel(const uint64_t *__restrict__ lwe_in, int n, const uint64_t *__restrict__ lut,
               const cplx *__restrict__ bsk, uint64_t *__restrict__ out, long B, uint64_t body_add,
-              uint64_t out_add, const cplx *__restrict__ twist, const cplx *__restrict__ untwist,
-              const cplx *__restrict__ wtab) {
+              uint64_t out_add, const cplx *__restrict__ wtab, const double *__restrict__ lf) {
     static_assert(BLOG <= 7, "digits are stored as int8");
+    static_assert(LEV == 6 && BLOG == 7, "the fused-twiddle transform's BSK rescale is the 8-bit model's");
     static_assert(LEV % LP == 0 && LP * K1 <= THREADS / 64, "one wave per FFT job of a pass");
     constexpr int LOGN = 10, JOBS = LP * K1, NPAIR = K1 * M;
     extern __shared__ __align__(16) unsigned char smem[];
     uint64_t *acc = reinterpret_cast<uint64_t *>(smem);           // [K1][N]
     cplx *buf = reinterpret_cast<cplx *>(acc + K1 * N);           // [JOBS][BUF_STRIDE], job = (lh, p)
-    cplx *s_tw = buf + JOBS * BUF_STRIDE;                         // twist
-    cplx *s_w = s_tw + M;                                         // W_512
-    cplx *s_utw = s_w + M;                                        // untwist
-    cplx *s_w0 = s_utw + M;                                       // [k - 1][t] = W_512^{t k}
-    cplx *s_w1 = s_w0 + 7 * 64;                                   // [k - 1][uu] = W_512^{8 uu k}
-    uint16_t *s_dig = reinterpret_cast<uint16_t *>(s_w1 + 7 * 8);  // [LEV][K1][M]: digit(j) | digit(j + M) << 8
+    double *s_lf = reinterpret_cast<double *>(buf + JOBS * BUF_STRIDE);  // lf1k.hpp's table
+    const cplx *s_untw = reinterpret_cast<const cplx *>(s_lf + lf1k::UNTW);
+    uint16_t *s_dig = reinterpret_cast<uint16_t *>(s_lf + lf1k::KERNEL_DOUBLES);  // [LEV][K1][M]: digit(j) | digit(j + M) << 8
     const long ct = blockIdx.x;
     if (ct >= B) return;  // whole workgroup
     const int tid = threadIdx.x;
@@ -81,13 +79,7 @@ __global__ void __launch_bounds__(THREADS, 1)
     const int jlh = fjob ? jb / K1 : 0, jp = fjob ? jb - (jb / K1) * K1 : 0;
     const uint64_t *in = lwe_in + (size_t)ct * (n + 1);
 
-    for (int i = tid; i < M; i += THREADS) {
-        s_tw[i] = twist[i];
-        s_w[i] = wtab[i];
-        s_utw[i] = untwist[i];
-    }
-    for (int i = tid; i < 7 * 64; i += THREADS) s_w0[i] = wtab[(i & 63) * ((i >> 6) + 1)];
-    if (tid < 7 * 8) s_w1[tid] = wtab[8 * (tid & 7) * ((tid >> 3) + 1)];
+    for (int i = tid; i < lf1k::KERNEL_DOUBLES; i += THREADS) s_lf[i] = lf[i];
     {
         const int bt = mod_switch(in[n] + body_add, LOGN);
         const int e0 = (2 * N - (bt % (2 * N))) % (2 * N);
@@ -161,47 +153,40 @@ __global__ void __launch_bounds__(THREADS, 1)
             if (fjob) {
                 int t = tq & 63;  // per pass: addresses derived from it are not kept across phases
                 asm volatile("" : "+v"(t));
-                const cplx w81 = s_w[64], w83 = s_w[192];  // W8^1, W8^3 (re-read: kept, they spill)
                 const int lev = lev0 - jlh;
                 const uint16_t *dg = s_dig + ((lev - 1) * K1 + jp) * M;
                 cplx *X = buf + jb * BUF_STRIDE;
                 cplx v[8];
-                // pass 0: twist, DFT8 over m, w[t kk] -> position t + 64 kk
+                // fused pass 0 (lf1k::pass0) -> position t + 64 kk
+                {
+                    int dr[8], di[8];
 #pragma unroll
-                for (int m = 0; m < 8; m++) {
-                    const uint32_t w = dg[t + 64 * m];
-                    const double a0 = (double)(int8_t)(w & 0xFF), a1 = (double)(int8_t)(w >> 8);
-                    const cplx tw = s_tw[t + 64 * m];
-                    v[m] = {fma(a0, tw.re, -(a1 * tw.im)), fma(a0, tw.im, a1 * tw.re)};
+                    for (int m = 0; m < 8; m++) {
+                        const uint32_t w = dg[t + 64 * m];
+                        dr[m] = (int8_t)(w & 0xFF);
+                        di[m] = (int8_t)(w >> 8);
+                    }
+                    lf1k::pass0(dr, di, v, lf1k::p0(lf));
                 }
-                dft8<false>(v, w81, w83);
                 br1024::s_setprio_c<2>();
-                X[pidx(t)] = v[0];
 #pragma unroll
-                for (int kk = 1; kk < 8; kk++) {
-                    const cplx tv = cmul(v[kk], s_w0[(kk - 1) * 64 + t]);
-                    X[pidx(t + 64 * kk)] = tv;  // W^0 = 1 exactly: only the sign of a zero can differ from skipping it
-                }
+                for (int kk = 0; kk < 8; kk++) X[pidx(t + 64 * kk)] = v[kk];
                 wave_sync();
-                // pass 1: points 64 gg + uu + 8 m, w[8 uu kk]
+                // fused pass 1: points 64 gg + uu + 8 m
                 {
                     const int gg = t >> 3, uu = t & 7;
 #pragma unroll
                     for (int m = 0; m < 8; m++) v[m] = X[pidx(64 * gg + uu + 8 * m)];
-                    dft8<false>(v, w81, w83);
+                    lf1k::dft8<false>(v, lf1k::k8(s_lf, lf1k::F1, 8, gg));
                     br1024::s_setprio_c<1>();
-                    X[pidx(64 * gg + uu)] = v[0];
 #pragma unroll
-                    for (int kk = 1; kk < 8; kk++) {
-                        const cplx tv = cmul(v[kk], s_w1[(kk - 1) * 8 + uu]);
-                        X[pidx(64 * gg + uu + 8 * kk)] = tv;  // W^0 = 1 exactly: only the sign of a zero can differ from skipping it
-                    }
+                    for (int kk = 0; kk < 8; kk++) X[pidx(64 * gg + uu + 8 * kk)] = v[kk];
                 }
                 wave_sync();
-                // pass 2: points 8 t + m, no twiddles
+                // fused pass 2: points 8 t + m
 #pragma unroll
                 for (int m = 0; m < 8; m++) v[m] = X[pidx(8 * t + m)];
-                dft8<false>(v, w81, w83);
+                lf1k::dft8<false>(v, lf1k::k8(s_lf, lf1k::F2, 64, t));
 #pragma unroll
                 for (int kk = 0; kk < 8; kk++) X[pidx(8 * t + kk)] = v[kk];
             }
@@ -253,7 +238,7 @@ __global__ void __launch_bounds__(THREADS, 1)
         if (jb < K1) {
             int t = tq & 63;
             asm volatile("" : "+v"(t));
-            const cplx w81 = s_w[64], w83 = s_w[192];
+            const cplx w81 = wtab[64], w83 = wtab[192];
             cplx *Y = buf + jb * BUF_STRIDE;
             cplx v[8];
 #pragma unroll
@@ -264,26 +249,16 @@ __global__ void __launch_bounds__(THREADS, 1)
             wave_sync();
             {
                 const int gg = t >> 3, uu = t & 7;
-                v[0] = Y[pidx(64 * gg + uu)];
 #pragma unroll
-                for (int kk = 1; kk < 8; kk++) {
-                    const cplx y = Y[pidx(64 * gg + uu + 8 * kk)];
-                    const cplx tv = cmul(y, cconj(s_w1[(kk - 1) * 8 + uu]));
-                    v[kk] = tv;  // W^0 = 1 exactly: only the sign of a zero can differ from skipping it
-                }
-                dft8<true>(v, w81, w83);
+                for (int kk = 0; kk < 8; kk++) v[kk] = Y[pidx(64 * gg + uu + 8 * kk)];
+                lf1k::dft8<true>(v, lf1k::k8(s_lf, lf1k::I1, 8, uu));
 #pragma unroll
                 for (int m = 0; m < 8; m++) Y[pidx(64 * gg + uu + 8 * m)] = v[m];
             }
             wave_sync();
-            v[0] = Y[pidx(t)];
 #pragma unroll
-            for (int kk = 1; kk < 8; kk++) {
-                const cplx y = Y[pidx(t + 64 * kk)];
-                const cplx tv = cmul(y, cconj(s_w0[(kk - 1) * 64 + t]));
-                v[kk] = tv;  // W^0 = 1 exactly: only the sign of a zero can differ from skipping it
-            }
-            dft8<true>(v, w81, w83);
+            for (int kk = 0; kk < 8; kk++) v[kk] = Y[pidx(t + 64 * kk)];
+            lf1k::dft8<true>(v, lf1k::k8(s_lf, lf1k::I0, 64, t));
             wave_sync();  // this wave's reads of Y precede its writes below (LDS executes in order)
 #pragma unroll
             for (int m = 0; m < 8; m++) Y[t + 64 * m] = v[m];  // coefficient pair j = t + 64 m
@@ -293,13 +268,13 @@ __global__ void __launch_bounds__(THREADS, 1)
         // inverse waves' VALU work): item i = (q, j), wave-uniform q ----
         for (int i = tid; i < K1 * M; i += THREADS) {
             const int q = i >> 9, j = i & (M - 1);
-            const cplx tt = cmul(buf[q * BUF_STRIDE + j], s_utw[j]);
+            const cplx tt = cmul(buf[q * BUF_STRIDE + j], s_untw[j]);  // conj(twist); 2^-9 in the exponent
             uint64_t *poly = acc + q * N;
             bool o0, o1;
-            uint64_t a0 = torus_add_fast(tt.re, poly[j], o0), a1 = torus_add_fast(tt.im, poly[j + M], o1);
+            uint64_t a0 = torus_add_fast_sh<9>(tt.re, poly[j], o0), a1 = torus_add_fast_sh<9>(tt.im, poly[j + M], o1);
             if (__builtin_amdgcn_ballot_w64(!(o0 && o1))) {  // zeros, out-of-range magnitudes (rare)
-                a0 = poly[j] + from_torus_bits(tt.re);
-                a1 = poly[j + M] + from_torus_bits(tt.im);
+                a0 = poly[j] + from_torus_bits(tt.re * 0x1p-9);
+                a1 = poly[j + M] + from_torus_bits(tt.im * 0x1p-9);
             }
             poly[j] = a0;
             poly[j + M] = a1;

@@ -335,6 +335,49 @@ std::vector<double> make_lf512_table() {
     return t;
 }
 
+// ... for N = 1024 (lf1k.hpp layout; the oracle's or_lf1k_plan_build): angles 2 pi num / 2048, a fused DFT8
+// of ratio g = (cos, tan) of g^4, g^2, g W8^-+k1 as 6 chunks of 2 doubles, chunk-major per table
+std::vector<double> make_lf1k_table() {
+    std::vector<double> t(3788, 0.0);
+    auto ct = [&](long num, double *o) {
+        double c, s;
+        sincos_2pi(num, 2048, c, s);
+        o[0] = c;
+        o[1] = s / c;
+    };
+    auto k8 = [&](int off, int n, int idx, long num, bool inv) {
+        double e[12];
+        ct(4 * num, &e[0]);
+        ct(2 * num, &e[2]);
+        for (int k1 = 0; k1 < 4; k1++) ct(num + (inv ? 256 : -256) * k1, &e[4 + 2 * k1]);
+        for (int q = 0; q < 6; q++) {
+            t[off + 2 * (q * n + idx)] = e[2 * q];
+            t[off + 2 * (q * n + idx) + 1] = e[2 * q + 1];
+        }
+    };
+    t[0] = 1.0 / std::sqrt(2.0);
+    ct(128, &t[1]);
+    for (int k1 = 0; k1 < 4; k1++) ct(64 - 256 * k1, &t[4 + 2 * k1]);
+    for (int g = 0; g < 8; g++) {
+        k8(12, 8, g, 8 - 32 * g, false);   // F1
+        k8(876, 8, g, 1 + 32 * g, true);   // I1
+    }
+    for (int l = 0; l < 64; l++) {
+        k8(108, 64, l, 1 - 4 * (l >> 3) - 32 * (l & 7), false);  // F2
+        k8(972, 64, l, 1 + 4 * l, true);                          // I0
+    }
+    for (int j = 0; j < 512; j++) {
+        double c, s;
+        sincos_2pi(j, 2048, c, s);
+        t[1740 + 2 * j] = c;
+        t[1740 + 2 * j + 1] = -s;
+        sincos_2pi(-((j >> 6) + ((j >> 3) & 7)), 2048, c, s);
+        t[2764 + 2 * j] = c;
+        t[2764 + 2 * j + 1] = s;
+    }
+    return t;
+}
+
 FftTables make_fft_tables(int N) {
     FftTables t;
     t.N = N;

@@ -126,5 +126,6 @@ struct FftTables {
 };
 FftTables make_fft_tables(int N);
 std::vector<double> make_lf512_table();  // lf512.hpp layout
+std::vector<double> make_lf1k_table();   // lf1k.hpp layout
 
 }  // namespace tae

@@ -217,19 +217,19 @@ class Engine {
     void prepare_mfma_keys();
     // batched N=1024, k=2 blind rotation (br1024.hpp) for this set's (levels, base_log), or nullptr
     void (*br1024_pbs_)(const uint64_t *, int, const uint64_t *, int, const cplx *, int, uint64_t *, long, uint64_t,
-                        uint64_t, const cplx *, const cplx *, const cplx *, uint64_t *) = nullptr;
+                        uint64_t, const cplx *, const cplx *, const cplx *, const double *, uint64_t *) = nullptr;
     decltype(br1024_pbs_) br1024_vp_ = nullptr;
     decltype(br1024_pbs_) br1024_pbs1_ = nullptr;  // one ciphertext per workgroup (small batches)
     int br1024_pbs1_lp_ = 1;                       // its levels per pass
-    bool br1024s_ = false;                         // br1024s.hpp for two ciphertexts per workgroup
+    bool lf1k_ = false;                            // the 8-bit model's PBS: the N = 1024 fused transform (lf1k.hpp)
     // latency blind rotation, one ciphertext per 1024-thread workgroup (br1024lat.hpp), or nullptr
     void (*br1024lat_)(const uint64_t *, int, const uint64_t *, const cplx *, uint64_t *, long, uint64_t, uint64_t,
-                       const cplx *, const cplx *, const cplx *) = nullptr;
+                       const cplx *, const double *) = nullptr;
     size_t br1024lat_lds_ = 0;
     bool x4_512_ = false;     // N = 512, k = 4 (lvl_64): batched blind rotations br512x4 / br512lat
     long lat_max_ = 256;      // batch size up to which br512lat runs (TAE_BR_LAT_MAX)
     int num_cu_ = 256;
-    double *d_lf_ = nullptr;  // the fused-twiddle transform's table (lf512.hpp), params_sqrd_lvl_64
+    double *d_lf_ = nullptr;  // the fused-twiddle transform's table (lf512.hpp: params_sqrd_lvl_64, lf1k.hpp: 8-bit)
     bool timing_ = false, clock_ = false;
     uint64_t *d_clk_ = nullptr;
     size_t cap_clk_ = 0;

@@ -23,7 +23,6 @@
 #include "br512lat.hpp"
 #include "br1024.hpp"
 #include "br1024lat.hpp"
-#include "br1024s.hpp"
 #include "ksgemm.hpp"
 #include "engine.hpp"
 #include "fft_device.hpp"
@@ -620,14 +619,13 @@ __global__ void s1_gather_kernel(const uint64_t *__restrict__ in, uint64_t *__re
     }
 }
 
-// the Fourier BSK the fused-twiddle transform multiplies with (lf512.hpp): G * conj(E2(pos)) per
-// position, the oracle's lf_rescale (same cmul)
-__global__ void __launch_bounds__(kThreads) lf_rescale_kernel(cplx *__restrict__ g, size_t polys,
-                                                              const double *__restrict__ lf) {
-    const cplx *e2 = reinterpret_cast<const cplx *>(lf + lf512::E2);
-    const size_t total = polys * 256;
+// the Fourier BSK the fused-twiddle transforms multiply with (lf512.hpp, lf1k.hpp): G * conj(E2(pos)) per
+// position (M = 256 or 512 positions), the oracle's lf_rescale (same cmul)
+__global__ void __launch_bounds__(kThreads) lf_rescale_kernel(cplx *__restrict__ g, size_t polys, int M,
+                                                              const cplx *__restrict__ e2) {
+    const size_t total = polys * M;
     for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x)
-        g[t] = cmul(g[t], e2[t & 255]);
+        g[t] = cmul(g[t], e2[t & (M - 1)]);
 }
 
 unsigned grid_for(size_t total) { return (unsigned)std::min<size_t>((total + kThreads - 1) / kThreads, 65536); }
@@ -746,8 +744,10 @@ void Engine::init_common() {
     // small ones.  TAE_BR_LAT_MAX (a tuning knob, both sides pinned by tests) is the batch size up
     // to which br512lat runs (0: never).
     x4_512_ = p_.N == 512 && p_.k == 4 && p_.pbs_l == 3 && p_.pbs_b == 12 && p_.cbs_l == 1 && p_.cbs_b == 13;
-    if (x4_512_) {  // the blind rotations' fused-twiddle transform (lf512.hpp)
-        const std::vector<double> lf = make_lf512_table();
+    // the 8-bit model's set: its PBS blind rotations run the N = 1024 fused-twiddle transform (lf1k.hpp)
+    lf1k_ = p_.N == 1024 && p_.k == 2 && p_.pbs_l == 6 && p_.pbs_b == 7;
+    if (x4_512_ || lf1k_) {  // the blind rotations' fused-twiddle transform (lf512.hpp / lf1k.hpp)
+        const std::vector<double> lf = x4_512_ ? make_lf512_table() : make_lf1k_table();
         d_lf_ = static_cast<double *>(alloc(lf.size() * 8));
         HIPC(hipMemcpy(d_lf_, lf.data(), lf.size() * 8, hipMemcpyHostToDevice));
     }
@@ -781,16 +781,7 @@ void Engine::init_common() {
         // one ciphertext per 1024-thread workgroup, three levels per pass (the 8-bit model's PBS;
         // TAE_B1K_LAT=0: br1024's one-ciphertext kernel instead)
         const char *blat = getenv("TAE_B1K_LAT");
-        // TAE_B1K_STREAM=1: two ciphertexts per workgroup with the FFT jobs streamed across the levels
-        // (br1024s.hpp; bit-exact, but 228.7 vs 226.7 ms per 8192-ciphertext launch on one box, so br1024's
-        // level-by-level kernel stays the default; profiles/r04_ab_b1ks_sgprsel.txt)
-        const char *bstr = getenv("TAE_B1K_STREAM");
-        if (p_.pbs_l == br1024s::LEV && p_.pbs_b == br1024s::BLOG && bstr && bstr[0] == '1') {
-            br1024s_ = true;
-            HIPC(hipFuncSetAttribute((const void *)br1024s::br_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)br1024s::lds_bytes()));
-        }
-        if (p_.pbs_l == 6 && p_.pbs_b == 7 && !(blat && blat[0] == '0')) {
+        if (lf1k_ && !(blat && blat[0] == '0')) {
             br1024lat_ = br1024lat::br_kernel<6, 7, 3>;
             br1024lat_lds_ = br1024lat::lds_bytes<6, 7, 3>();
             HIPC(hipFuncSetAttribute((const void *)br1024lat_, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -826,8 +817,9 @@ void Engine::bsk_to_fourier(const uint64_t *d_bsk_std) {
             d_bsk_std, d_bsk_f_, polys, d_twist_, d_w_);
     }
     HIPC(hipGetLastError());
-    if (x4_512_) {  // the blind rotations run the fused-twiddle transform: its BSK carries conj(E2)
-        lf_rescale_kernel<<<grid_for(polys * 256), kThreads, 0, stream_>>>(d_bsk_f_, polys, d_lf_);
+    if (x4_512_ || lf1k_) {  // the blind rotations run the fused-twiddle transform: its BSK carries conj(E2)
+        const cplx *e2 = reinterpret_cast<const cplx *>(d_lf_ + (x4_512_ ? lf512::E2 : lf1k::E2));
+        lf_rescale_kernel<<<grid_for(polys * M), kThreads, 0, stream_>>>(d_bsk_f_, polys, M, e2);
         HIPC(hipGetLastError());
     }
     HIPC(hipStreamSynchronize(stream_));
@@ -1032,7 +1024,7 @@ void Engine::bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint
     }
     if (br1024lat_ && (long)B <= (long)num_cu_) {
         br1024lat_<<<(unsigned)B, br1024lat::THREADS, br1024lat_lds_, stream_>>>(
-            d_small, p_.n, d_lut_glwe, d_bsk_f_, d_big, (long)B, body_add, out_add, d_twist_, d_untwist_, d_w_);
+            d_small, p_.n, d_lut_glwe, d_bsk_f_, d_big, (long)B, body_add, out_add, d_w_, d_lf_);
         HIPC(hipGetLastError());
         return;
     }
@@ -1041,17 +1033,10 @@ void Engine::bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint
         const int C = (long)B <= (long)num_cu_ ? 1 : 2;
         const size_t wgs = (B + C - 1) / C;
         uint64_t *clk = C == 2 ? clock_buffer(wgs) : nullptr;  // the throughput instantiation only
-        if (C == 2 && br1024s_) {
-            br1024s::br_kernel<<<(unsigned)wgs, br1024s::THREADS, br1024s::lds_bytes(), stream_>>>(
-                d_small, p_.n, d_lut_glwe, d_bsk_f_, d_big, (long)B, body_add, out_add, d_twist_, d_w_, clk);
-            HIPC(hipGetLastError());
-            record_clock(clk, wgs);
-            return;
-        }
-        (C == 1 ? br1024_pbs1_ : br1024_pbs_)<<<(unsigned)wgs, br1024::THREADS, br1024::lds_bytes(C, C == 1 ? br1024_pbs1_lp_ : 1),
-                                                              stream_>>>(
+        (C == 1 ? br1024_pbs1_ : br1024_pbs_)<<<(unsigned)wgs, br1024::THREADS,
+                                                 br1024::lds_bytes(C, C == 1 ? br1024_pbs1_lp_ : 1, lf1k_), stream_>>>(
             d_small, p_.n, d_lut_glwe, 0, d_bsk_f_, 0, d_big, (long)B, body_add, out_add, d_twist_, d_untwist_, d_w_,
-            clk);
+            d_lf_, clk);
         HIPC(hipGetLastError());
         record_clock(clk, wgs);
         return;
@@ -1209,7 +1194,8 @@ void Engine::vertical_packing(const cplx *d_ggsw_f, size_t G, int n_in, const ui
     if (br1024_vp_) {
         const size_t wgs = G * (size_t)((n_out + 1) / 2);
         br1024_vp_<<<(unsigned)wgs, br1024::THREADS, br1024::lds_bytes(2), stream_>>>(
-            nullptr, 0, d_lut, n_out, d_ggsw_f, n_in, d_out, (long)G, 0, 0, d_twist_, d_untwist_, d_w_, nullptr);
+            nullptr, 0, d_lut, n_out, d_ggsw_f, n_in, d_out, (long)G, 0, 0, d_twist_, d_untwist_, d_w_, nullptr,
+            nullptr);
         HIPC(hipGetLastError());
         return;
     }
