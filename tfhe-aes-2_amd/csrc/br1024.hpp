@@ -239,11 +239,7 @@ __global__ void __launch_bounds__(THREADS, 1)
     cplx gv[LP * K1 * K1];
     BPROF_DECL
     for (int step = 0; step < steps; step++) {
-#if TAE_B1K_PV == 2
-        s_setprio_c<3>();
-#else
         s_setprio_c<2>();
-#endif
         int e, gstep;
         if (PBS) {
             const uint64_t a = a_next;
@@ -295,8 +291,6 @@ __global__ void __launch_bounds__(THREADS, 1)
         for (int a = 0; a < K1 * C; a++) accr[a] = cplx{0.0, 0.0};
 
         BPROF(0);
-        uint32_t dsel[8];
-        (void)dsel;
         for (int lev0 = LEV; lev0 >= 1; lev0 -= LP) {
 #pragma unroll
             for (int lh = 0; lh < LP; lh++)
@@ -316,27 +310,6 @@ __global__ void __launch_bounds__(THREADS, 1)
                     // fused pass 0 (lf1k::pass0) of the level's digits -> position t + 64 kk
                     int dr[8], di[8];
                     const int wsel = (lev - 1) >> 1, sh = ((lev - 1) & 1) * 16;
-#ifdef TAE_B1K_DSEL
-                    // the digit word of a level pair, selected once for both levels (LP = 1: levels descend,
-                    // the even one first)
-                    if (LP > 1 || !(lev & 1)) {
-#pragma unroll
-                        for (int m = 0; m < 8; m++) {
-                            uint32_t dw = dig[0][m];
-#pragma unroll
-                            for (int w = 1; w < DW; w++) {
-                                const uint32_t msk = 0u - (uint32_t)(wsel == w);
-                                dw = (dw & ~msk) | (dig[w][m] & msk);
-                            }
-                            dsel[m] = dw;
-                        }
-                    }
-#pragma unroll
-                    for (int m = 0; m < 8; m++) {
-                        dr[m] = __builtin_amdgcn_sbfe(dsel[m], sh, 8);
-                        di[m] = __builtin_amdgcn_sbfe(dsel[m], sh + 8, 8);
-                    }
-#else
 #pragma unroll
                     for (int m = 0; m < 8; m++) {
                         uint32_t dw = dig[0][m];
@@ -348,7 +321,6 @@ __global__ void __launch_bounds__(THREADS, 1)
                         dr[m] = __builtin_amdgcn_sbfe(dw, sh, 8);
                         di[m] = __builtin_amdgcn_sbfe(dw, sh + 8, 8);
                     }
-#endif
                     lf1k::pass0(dr, di, v, k0);
 #pragma unroll
                     for (int kk = 0; kk < 8; kk++) X[pidx(tt + 64 * kk)] = v[kk];
@@ -391,13 +363,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                 }
                 }
                 wave_sync();
-#if TAE_B1K_PV == 1
-                s_setprio_c<2>();
-#elif TAE_B1K_PV == 4
-                s_setprio_c<1>();
-#else
                 if (lev0 == LEV) s_setprio_c<1>(); else s_setprio_c<2>();
-#endif
                 // pass 1: points 64 gg + uu + 8 m, w[8 uu kk]
                 {
                     const int gg = tt >> 3, uu = tt & 7;
@@ -418,13 +384,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                     }
                 }
                 wave_sync();
-#if TAE_B1K_PV == 1
-                s_setprio_c<1>();
-#elif TAE_B1K_PV == 4
-                s_setprio_c<0>();
-#else
                 if (lev0 == LEV) s_setprio_c<0>(); else s_setprio_c<1>();
-#endif
                 // pass 2: points 8 t + m, no twiddles
 #pragma unroll
                 for (int m = 0; m < 8; m++) v[m] = X[pidx(8 * tt + m)];
@@ -481,9 +441,6 @@ __global__ void __launch_bounds__(THREADS, 1)
 #pragma unroll
             for (int m = 0; m < 8; m++) Y[pidx(8 * tt + m)] = v[m];
             wave_sync();
-#if TAE_B1K_PV == 3
-            s_setprio_c<2>();
-#endif
             // inverse pass 1: conj(w[8 uu kk]) on points 64 gg + uu + 8 kk
             {
                 const int gg = tt >> 3, uu = tt & 7;
@@ -505,11 +462,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                 for (int m = 0; m < 8; m++) Y[pidx(64 * gg + uu + 8 * m)] = v[m];
             }
             wave_sync();
-#if TAE_B1K_PV == 3
-            s_setprio_c<1>();
-#else
             s_setprio_c<2>();
-#endif
             // inverse pass 0: conj(w[t kk]) on points t + 64 kk, untwist, from_torus, ACC +=
             if constexpr (LFT) {
 #pragma unroll
