@@ -13,4 +13,4 @@ cat $OUT/kt_bench.json
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 $ROOT/bench.py $ARGS > /dev/null 2> $OUT/pmc_fetch.err || { echo "fetch rc=$?"; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 $ROOT/bench.py $ARGS > /dev/null 2> $OUT/pmc_write.err || { echo "write rc=$?"; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY --output-format csv -d $OUT/pmc_sq -o run -- python3 $ROOT/bench.py $ARGS > /dev/null 2> $OUT/pmc_sq.err || { echo "sq rc=$?"; exit 1; }
-echo done
+python3 $ROOT/scripts/prof_split_summary.py $OUT $OUT/prof8_summary.json > /dev/null 2>&1 && echo done
