@@ -799,6 +799,54 @@ void *or_lf1k_plan_new(void) {
 }
 void or_lf1k_e2(const void *plan, or_c64 *e2) { memcpy(e2, ((const lf1k_plan *)plan)->e2, sizeof(or_c64) * 512); }
 
+/* the plans' constants in the product's table layouts (lf512.hpp / lf1k.hpp), for
+ * tests/native/lf_tables_test.cpp, which compares them with the product's own tables bit for bit */
+void or_lf_table(const void *plan, double *t /*[1700]*/) {
+    const lf_plan *P = (const lf_plan *)plan;
+    memset(t, 0, sizeof(double) * 1700);
+    for (int k = 0; k < 4; k++) {
+        memcpy(t + 4 * k, &P->fa2[k], sizeof(lf4));
+        memcpy(t + 336 + 4 * k, &P->ib2[k], sizeof(lf4));
+    }
+    for (int a = 0; a < 16; a++) {
+        memcpy(t + 16 + 4 * a, &P->fb1[a], sizeof(lf4));
+        memcpy(t + 352 + 4 * a, &P->ia1[a], sizeof(lf4));
+        for (int l = 0; l < 4; l++) {
+            memcpy(t + 80 + 4 * (4 * a + l), &P->fb2[4 * a + l], sizeof(lf4));
+            memcpy(t + 416 + 4 * (4 * a + l), &P->ia2[4 * a + l], sizeof(lf4));
+        }
+    }
+    t[672] = P->s2;
+    t[673] = P->c8;
+    t[674] = P->t8;
+    memcpy(t + 676, P->untw, sizeof(or_c64) * 256);
+    memcpy(t + 1188, P->e2, sizeof(or_c64) * 256);
+}
+static void lf1k_put(double *t, int off, int n, int idx, const double *e) {
+    for (int q = 0; q < 6; q++) {
+        t[off + 2 * (q * n + idx)] = e[2 * q];
+        t[off + 2 * (q * n + idx) + 1] = e[2 * q + 1];
+    }
+}
+void or_lf1k_table(const void *plan, double *t /*[3788]*/) {
+    const lf1k_plan *P = (const lf1k_plan *)plan;
+    memset(t, 0, sizeof(double) * 3788);
+    t[0] = P->s2;
+    t[1] = P->c8;
+    t[2] = P->t8;
+    memcpy(t + 4, P->p0, sizeof(double) * 8);
+    for (int g = 0; g < 8; g++) {
+        lf1k_put(t, 12, 8, g, P->f1[g]);
+        lf1k_put(t, 876, 8, g, P->i1[g]);
+    }
+    for (int l = 0; l < 64; l++) {
+        lf1k_put(t, 108, 64, l, P->f2[l]);
+        lf1k_put(t, 972, 64, l, P->i0[l]);
+    }
+    memcpy(t + 1740, P->untw, sizeof(or_c64) * 512);
+    memcpy(t + 2764, P->e2, sizeof(or_c64) * 512);
+}
+
 /* either plan (the tag is its first member) */
 static int lf_plan_n(const void *plan) { return *(const int *)plan; }
 void or_lf_any_free(void *plan) {

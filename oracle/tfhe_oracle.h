@@ -97,6 +97,9 @@ void or_lf1k_fwd(const void *plan, const int64_t *poly, or_c64 *X);
 void or_lf1k_bwd_add(const void *plan, const or_c64 *Y, uint64_t *out);
 void or_lf1k_e2(const void *plan, or_c64 *e2 /*[512]*/);
 void or_lf_any_free(void *plan);
+/* the constants in the product's table layouts (tests/native/lf_tables_test.cpp) */
+void or_lf_table(const void *plan, double *t /*[1700]*/);
+void or_lf1k_table(const void *plan, double *t /*[3788]*/);
 void or_fft_raw_fwd(const or_fft *f, or_c64 *z);
 void or_fft_raw_inv(const or_fft *f, or_c64 *z);
 

@@ -40,6 +40,15 @@ static void check_ft(double x) {
             printf("torus_add_fast_sh<8>(%a): ok %d got %016llx want %016llx\n", y, (int)ok8,
                    (unsigned long long)(a8 - acc0), (unsigned long long)b);
     }
+    // ... and of y = x 2^9 (lf1k.hpp, N = 1024)
+    {
+        const double y = x * 0x1p9;
+        bool ok9;
+        const uint64_t a9 = tae::torus_add_fast_sh<9>(y, acc0, ok9);
+        if ((ok9 != ok || (ok9 && a9 != acc)) && fails++ < 10)
+            printf("torus_add_fast_sh<9>(%a): ok %d got %016llx want %016llx\n", y, (int)ok9,
+                   (unsigned long long)(a9 - acc0), (unsigned long long)b);
+    }
     // the kernels' fallback undoes the fast value (linear in acc) and adds the exact one
     bool d;
     if (acc - tae::torus_add_fast(x, 0, d) + b != acc0 + b && fails++ < 10)
