@@ -58,17 +58,15 @@ def test_pbs_shift_boolean8_bit_exact(gpu_context8, oracle_keys8, client8, level
         assert min(err, (1 << 64) - err) < 1 << (63 - 6 * level), (i, level)  # within alpha
 
 
-@pytest.mark.parametrize("lat,pair,rounds,B", [("1", "1", "0", 5), ("0", "1", "0", 5), ("0", "0", "0", 5),
-                                               ("1", "1", "0", 300), ("1", "1", "1", 300), ("1", "1", "0", 513),
-                                               ("1", "1", "1", 513)])
-def test_pbs8_kernel_variants_bit_exact(product_raw8, oracle_keys8, client8, lat, pair, rounds, B):
+@pytest.mark.parametrize("lat,pair,B", [("1", "1", 5), ("0", "1", 5), ("0", "0", 5), ("1", "1", 300),
+                                        ("1", "1", 513)])
+def test_pbs8_kernel_variants_bit_exact(product_raw8, oracle_keys8, client8, lat, pair, B):
     """The N=1024 blind-rotation variants the engine picks, all on the fused-twiddle transform (lf1k.hpp,
     the oracle's or_lf1k_*): for batches up to one ciphertext per CU the 1024-thread latency kernel
     (br1024lat, default), or with TAE_B1K_LAT=0 br1024 with one ciphertext per workgroup and two levels
     per pass (or one: TAE_B1K_PAIR=0); and two ciphertexts per workgroup (B > the CU count, odd tail
-    workgroup of one): br1024's level-by-level kernel (default) or br1024r's rounds of eight FFT jobs
-    (TAE_B1K_ROUNDS=1)."""
-    env = {"TAE_B1K_LAT": lat, "TAE_B1K_PAIR": pair, "TAE_B1K_ROUNDS": rounds}
+    workgroup of one)."""
+    env = {"TAE_B1K_LAT": lat, "TAE_B1K_PAIR": pair}
     os.environ.update(env)
     try:
         ctx = tfhe_aes.context_from_raw(tfhe_aes.PARAMS_WOPPBS_8BIT, product_raw8[1], device=0)

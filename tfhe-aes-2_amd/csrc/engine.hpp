@@ -222,7 +222,6 @@ class Engine {
     decltype(br1024_pbs_) br1024_pbs1_ = nullptr;  // one ciphertext per workgroup (small batches)
     int br1024_pbs1_lp_ = 1;                       // its levels per pass
     bool lf1k_ = false;                            // the 8-bit model's PBS: the N = 1024 fused transform (lf1k.hpp)
-    bool br1024r_ = false;                         // its C = 2 PBS in rounds of eight FFT jobs (br1024r.hpp)
     // latency blind rotation, one ciphertext per 1024-thread workgroup (br1024lat.hpp), or nullptr
     void (*br1024lat_)(const uint64_t *, int, const uint64_t *, const cplx *, uint64_t *, long, uint64_t, uint64_t,
                        const cplx *, const double *) = nullptr;

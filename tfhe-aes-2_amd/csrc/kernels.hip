@@ -23,7 +23,6 @@
 #include "br512lat.hpp"
 #include "br1024.hpp"
 #include "br1024lat.hpp"
-#include "br1024r.hpp"
 #include "ksgemm.hpp"
 #include "engine.hpp"
 #include "fft_device.hpp"
@@ -781,15 +780,6 @@ void Engine::init_common() {
                                          (int)br1024::lds_bytes(2)));
         // one ciphertext per 1024-thread workgroup, three levels per pass (the 8-bit model's PBS;
         // TAE_B1K_LAT=0: br1024's one-ciphertext kernel instead)
-        // TAE_B1K_ROUNDS=1: two ciphertexts per workgroup with the step's 36 FFT jobs dealt out in rounds of
-        // eight (br1024r.hpp; bit-exact, but 231.7 vs 212.9 ms per 8192-ciphertext launch on one box:
-        // profiles/r04_ab_b1k_rounds.txt), else br1024's level-by-level C = 2 kernel
-        const char *brd = getenv("TAE_B1K_ROUNDS");
-        if (lf1k_ && brd && brd[0] == '1') {
-            br1024r_ = true;
-            HIPC(hipFuncSetAttribute((const void *)br1024r::br_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)br1024r::lds_bytes()));
-        }
         const char *blat = getenv("TAE_B1K_LAT");
         if (lf1k_ && !(blat && blat[0] == '0')) {
             br1024lat_ = br1024lat::br_kernel<6, 7, 3>;
@@ -1043,13 +1033,6 @@ void Engine::bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint
         const int C = (long)B <= (long)num_cu_ ? 1 : 2;
         const size_t wgs = (B + C - 1) / C;
         uint64_t *clk = C == 2 ? clock_buffer(wgs) : nullptr;  // the throughput instantiation only
-        if (C == 2 && br1024r_) {
-            br1024r::br_kernel<<<(unsigned)wgs, br1024r::THREADS, br1024r::lds_bytes(), stream_>>>(
-                d_small, p_.n, d_lut_glwe, d_bsk_f_, d_big, (long)B, body_add, out_add, d_w_, d_lf_, clk);
-            HIPC(hipGetLastError());
-            record_clock(clk, wgs);
-            return;
-        }
         (C == 1 ? br1024_pbs1_ : br1024_pbs_)<<<(unsigned)wgs, br1024::THREADS,
                                                  br1024::lds_bytes(C, C == 1 ? br1024_pbs1_lp_ : 1, lf1k_), stream_>>>(
             d_small, p_.n, d_lut_glwe, 0, d_bsk_f_, 0, d_big, (long)B, body_add, out_add, d_twist_, d_untwist_, d_w_,
