@@ -801,19 +801,25 @@ void or_lf1k_e2(const void *plan, or_c64 *e2) { memcpy(e2, ((const lf1k_plan *)p
 
 /* the plans' constants in the product's table layouts (lf512.hpp / lf1k.hpp), for
  * tests/native/lf_tables_test.cpp, which compares them with the product's own tables bit for bit */
+static void lf4_put(double *t, int off, int n, int idx, const lf4 *k) {
+    t[off + 2 * idx] = k->c2;
+    t[off + 2 * idx + 1] = k->t2;
+    t[off + 2 * (n + idx)] = k->c1;
+    t[off + 2 * (n + idx) + 1] = k->t1;
+}
 void or_lf_table(const void *plan, double *t /*[1700]*/) {
     const lf_plan *P = (const lf_plan *)plan;
     memset(t, 0, sizeof(double) * 1700);
     for (int k = 0; k < 4; k++) {
-        memcpy(t + 4 * k, &P->fa2[k], sizeof(lf4));
-        memcpy(t + 336 + 4 * k, &P->ib2[k], sizeof(lf4));
+        lf4_put(t, 0, 4, k, &P->fa2[k]);
+        lf4_put(t, 336, 4, k, &P->ib2[k]);
     }
     for (int a = 0; a < 16; a++) {
-        memcpy(t + 16 + 4 * a, &P->fb1[a], sizeof(lf4));
-        memcpy(t + 352 + 4 * a, &P->ia1[a], sizeof(lf4));
+        lf4_put(t, 16, 16, a, &P->fb1[a]);
+        lf4_put(t, 352, 16, a, &P->ia1[a]);
         for (int l = 0; l < 4; l++) {
-            memcpy(t + 80 + 4 * (4 * a + l), &P->fb2[4 * a + l], sizeof(lf4));
-            memcpy(t + 416 + 4 * (4 * a + l), &P->ia2[4 * a + l], sizeof(lf4));
+            lf4_put(t, 80, 64, a + 16 * l, &P->fb2[4 * a + l]);
+            lf4_put(t, 416, 64, a + 16 * l, &P->ia2[4 * a + l]);
         }
     }
     t[672] = P->s2;

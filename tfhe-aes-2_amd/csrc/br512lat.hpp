@@ -173,16 +173,16 @@ __global__ void __launch_bounds__(THREADS, 1)
             cplx v[4];
             lf512::a1(dw, v, lf_s2, lf_c8, lf_t8);
             br512::transpose4(v);
-            lf512::dft4<false>(v, lf512::k4(s_lf, lf512::FA2 + 4 * r));
+            lf512::dft4<false>(v, lf512::k4(s_lf, lf512::FA2, 4, r));
 #pragma unroll
             for (int k2 = 0; k2 < 4; k2++) dst[baseA + SG3[k2]] = v[k2];
             wave_sync();
             // pass B (row kappa = u): positions 16 u + r + 4 i, in place
 #pragma unroll
             for (int i = 0; i < 4; i++) v[i] = dst[baseB + SG1[i]];
-            lf512::dft4<false>(v, lf512::k4(s_lf, lf512::FB1 + 4 * u));
+            lf512::dft4<false>(v, lf512::k4(s_lf, lf512::FB1, 16, u));
             br512::transpose4(v);
-            lf512::dft4<false>(v, lf512::k4(s_lf, lf512::FB2 + 4 * (4 * u + r)));
+            lf512::dft4<false>(v, lf512::k4(s_lf, lf512::FB2, 64, lane));
 #pragma unroll
             for (int k2 = 0; k2 < 4; k2++) dst[baseB + SG1[k2]] = v[k2];
         }
@@ -234,15 +234,15 @@ __global__ void __launch_bounds__(THREADS, 1)
             for (int i = 0; i < 4; i++) v[i] = base[baseB + SG1[i]];
             dft4<true>(v[0], v[1], v[2], v[3]);
             br512::transpose4(v);
-            lf512::dft4<true>(v, lf512::k4(s_lf, lf512::IB2 + 4 * r));
+            lf512::dft4<true>(v, lf512::k4(s_lf, lf512::IB2, 4, r));
 #pragma unroll
             for (int k2 = 0; k2 < 4; k2++) base[baseB + SG1[k2]] = v[k2];
             wave_sync();
 #pragma unroll
             for (int i = 0; i < 4; i++) v[i] = base[baseA + SG3[i]];
-            lf512::dft4<true>(v, lf512::k4(s_lf, lf512::IA1 + 4 * u));
+            lf512::dft4<true>(v, lf512::k4(s_lf, lf512::IA1, 16, u));
             br512::transpose4(v);
-            lf512::dft4<true>(v, lf512::k4(s_lf, lf512::IA2 + 4 * (4 * u + r)));
+            lf512::dft4<true>(v, lf512::k4(s_lf, lf512::IA2, 64, lane));
             wave_sync();  // this wave's reads of base precede its writes below (LDS executes in order)
 #pragma unroll
             for (int k2 = 0; k2 < 4; k2++) base[ll + 64 * k2] = v[k2];  // coefficient pair j = ll + 64 k2

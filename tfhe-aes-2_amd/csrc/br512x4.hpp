@@ -319,7 +319,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                     cplx v[4];
                     lf512::a1(dw, v, lf_s2, lf_c8, lf_t8);
                     br512::transpose4(v);
-                    lf512::dft4<false>(v, lf512::k4(s_lf, lf512::FA2 + 4 * r));
+                    lf512::dft4<false>(v, lf512::k4(s_lf, lf512::FA2, 4, r));
                     if (lev == LEV) PRIO(2);
 #pragma unroll
                     for (int k2 = 0; k2 < 4; k2++) jbuf[baseA + SG3[k2]] = v[k2];
@@ -332,9 +332,9 @@ __global__ void __launch_bounds__(THREADS, 1)
                     cplx v[4];
 #pragma unroll
                     for (int i = 0; i < 4; i++) v[i] = jbuf[baseB + SG1[i]];
-                    lf512::dft4<false>(v, lf512::k4(s_lf, lf512::FB1 + 4 * u));
+                    lf512::dft4<false>(v, lf512::k4(s_lf, lf512::FB1, 16, u));
                     br512::transpose4(v);
-                    lf512::dft4<false>(v, lf512::k4(s_lf, lf512::FB2 + 4 * (4 * u + r)));
+                    lf512::dft4<false>(v, lf512::k4(s_lf, lf512::FB2, 64, lane));
                     PRIO(0);
 #pragma unroll
                     for (int k2 = 0; k2 < 4; k2++) jbuf[baseB + SG1[k2]] = v[k2];
@@ -416,7 +416,7 @@ __global__ void __launch_bounds__(THREADS, 1)
                 for (int i = 0; i < 4; i++) v[i] = jbuf[baseB + SG1[i]];
                 dft4<true>(v[0], v[1], v[2], v[3]);
                 br512::transpose4(v);
-                lf512::dft4<true>(v, lf512::k4(s_lf, lf512::IB2 + 4 * r));
+                lf512::dft4<true>(v, lf512::k4(s_lf, lf512::IB2, 4, r));
 #pragma unroll
                 for (int k2 = 0; k2 < 4; k2++) jbuf[baseB + SG1[k2]] = v[k2];
             }
@@ -427,9 +427,9 @@ __global__ void __launch_bounds__(THREADS, 1)
                 cplx v[4];
 #pragma unroll
                 for (int i = 0; i < 4; i++) v[i] = jbuf[baseA + SG3[i]];
-                lf512::dft4<true>(v, lf512::k4(s_lf, lf512::IA1 + 4 * u));
+                lf512::dft4<true>(v, lf512::k4(s_lf, lf512::IA1, 16, u));
                 br512::transpose4(v);
-                lf512::dft4<true>(v, lf512::k4(s_lf, lf512::IA2 + 4 * (4 * u + r)));
+                lf512::dft4<true>(v, lf512::k4(s_lf, lf512::IA2, 64, lane));
                 uint64_t *poly = acc + jb * ACC_STRIDE;
 #pragma unroll
                 for (int k2 = 0; k2 < 4; k2++) {

@@ -305,20 +305,20 @@ std::vector<double> make_lf512_table() {
         o[0] = c;
         o[1] = s / c;
     };
-    auto k4 = [&](int off, long num) {
-        ct(2 * num, &t[off]);
-        ct(num, &t[off + 2]);
+    auto k4 = [&](int off, int n, int idx, long num) {  // chunk-major [2][n][2]
+        ct(2 * num, &t[off + 2 * idx]);
+        ct(num, &t[off + 2 * (n + idx)]);
     };
     for (int k = 0; k < 4; k++) {
-        k4(0 + 4 * k, 16 - 64 * k);    // FA2
-        k4(336 + 4 * k, 1 + 64 * k);   // IB2
+        k4(0, 4, k, 16 - 64 * k);    // FA2
+        k4(336, 4, k, 1 + 64 * k);   // IB2
     }
     for (int a = 0; a < 16; a++) {
-        k4(16 + 4 * a, 4 - 16 * a);    // FB1
-        k4(352 + 4 * a, 4 + 16 * a);   // IA1
+        k4(16, 16, a, 4 - 16 * a);    // FB1
+        k4(352, 16, a, 4 + 16 * a);   // IA1
         for (int l = 0; l < 4; l++) {
-            k4(80 + 4 * (4 * a + l), 1 - 4 * a - 64 * l);   // FB2
-            k4(416 + 4 * (4 * a + l), 1 + 4 * a + 64 * l);  // IA2
+            k4(80, 64, a + 16 * l, 1 - 4 * a - 64 * l);   // FB2, entry = lane (kappa, l1)
+            k4(416, 64, a + 16 * l, 1 + 4 * a + 64 * l);  // IA2, entry = lane (u, m1)
         }
     }
     t[672] = 1.0 / std::sqrt(2.0);

@@ -43,7 +43,7 @@ struct K8 {
     double c[4], t[4];      // the butterflies: rho_k1 = g W8^-+k1
 };
 
-typedef double d2 __attribute__((ext_vector_type(2)));
+using lf512::d2;
 
 // entry idx of the [6][n] chunk-major table at off
 __device__ __forceinline__ K8 k8(const double *tab, int off, int n, int idx) {

@@ -21,13 +21,15 @@ namespace tae {
 namespace lf512 {
 
 // table (doubles): per-lane (cos, tan) pairs of g^2 and g for each fused stage, the lane-uniform
-// constants, conj(twist), conj(E2)
-constexpr int FA2 = 0;     // [4]  forward pass A stage 2, lane row k1
-constexpr int FB1 = 16;    // [16] forward pass B stage 1, lane column kappa
-constexpr int FB2 = 80;    // [64] forward pass B stage 2, lane (kappa, l1) = 4 kappa + l1
-constexpr int IB2 = 336;   // [4]  inverse pass B stage 2, lane row u1
-constexpr int IA1 = 352;   // [16] inverse pass A stage 1, lane column u
-constexpr int IA2 = 416;   // [64] inverse pass A stage 2, lane (u, m1) = 4 u + m1
+// constants, conj(twist), conj(E2).  The per-lane tables are chunk-major, [2][n entries][2 doubles] (chunk
+// 0: g^2, chunk 1: g), and the (kappa, l1) / (u, m1) ones are indexed by the lane u + 16 r itself, so that
+// every wave's ds_read_b128 of them is lane-contiguous (conflict-free) or a broadcast.
+constexpr int FA2 = 0;     // [2][4]  forward pass A stage 2, entry = lane row r (k1)
+constexpr int FB1 = 16;    // [2][16] forward pass B stage 1, entry = lane column u (kappa)
+constexpr int FB2 = 80;    // [2][64] forward pass B stage 2, entry = lane u + 16 r (kappa, l1)
+constexpr int IB2 = 336;   // [2][4]  inverse pass B stage 2, entry = r (u1)
+constexpr int IA1 = 352;   // [2][16] inverse pass A stage 1, entry = u
+constexpr int IA2 = 416;   // [2][64] inverse pass A stage 2, entry = lane u + 16 r (u, m1)
 constexpr int CONSTS = 672;  // 1/sqrt 2, cos pi/8, tan pi/8, 0
 constexpr int UNTW = 676;  // [256] cplx conj(twist[j])
 constexpr int E2 = 1188;   // [256] cplx conj(E2(pos))
@@ -37,10 +39,12 @@ constexpr int KERNEL_DOUBLES = E2;  // what the blind rotations stage in LDS
 struct K4 {
     double c2, t2, c1, t1;
 };
-__device__ __forceinline__ K4 k4(const double *tab, int off) {
-    K4 k;
-    __builtin_memcpy(&k, tab + off, sizeof(K4));
-    return k;
+typedef double d2 __attribute__((ext_vector_type(2)));
+// entry idx of the [2][n] chunk-major table at off
+__device__ __forceinline__ K4 k4(const double *tab, int off, int n, int idx) {
+    const d2 a = *reinterpret_cast<const d2 *>(tab + off + 2 * idx);
+    const d2 b = *reinterpret_cast<const d2 *>(tab + off + 2 * (n + idx));
+    return {a.x, a.y, b.x, b.y};
 }
 
 // x (1 + i t) and a + c t
