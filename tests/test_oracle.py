@@ -145,6 +145,31 @@ def test_lf1k_negacyclic_product_within_bound(oracle_mod):
         assert e_lf < 4 * max(e_std, 1) and e_lf < 2**16
 
 
+@pytest.mark.parametrize("N,dmax", [(512, 2048), (1024, 64)])
+def test_lf_transforms_extreme_digits(oracle_mod, N, dmax):
+    """Both fused transforms on the decompositions' extreme digits (every coefficient +-base/2, alternating
+    and constant patterns, single spikes): forward within 1e-12 relative of the radix schedule, and the
+    external-product arithmetic against the exact negacyclic product inside the radix schedule's bound."""
+    F, T = oracle_mod.FFT(N), oracle_mod.LfTransform(N)
+    e2 = T.conj_e2()
+    rng = np.random.default_rng(N + dmax)
+    pats = [np.full(N, dmax), np.full(N, -dmax), np.where(np.arange(N) % 2 == 0, dmax, -dmax),
+            np.where(np.arange(N) < N // 2, dmax, -dmax), np.eye(1, N, 0)[0] * dmax, np.eye(1, N, N - 1)[0] * -dmax,
+            rng.choice([-dmax, dmax], size=N)]
+    for d in pats:
+        d = d.astype(np.int64)
+        x_lf, x_std = T.fwd_int(d), F.fwd_int(d)
+        assert np.max(np.abs(x_lf - x_std)) <= 1e-12 * max(np.max(np.abs(x_std)), 1.0)
+        a = rng.integers(0, 2**64 - 1, size=N, dtype=np.uint64)
+        exact = oracle_mod.negacyclic_mul_exact(a, d)
+        out, ref = np.zeros(N, dtype=np.uint64), np.zeros(N, dtype=np.uint64)
+        T.add_bwd_torus(F.fwd_torus(a) * e2 * x_lf, out)
+        F.add_bwd_torus(F.fwd_torus(a) * x_std, ref)
+        err = np.max(np.abs((out - exact).astype(np.int64)))
+        err_std = np.max(np.abs((ref - exact).astype(np.int64)))
+        assert err < 2**40 and err <= 4 * max(err_std, 1)
+
+
 def test_generate_luts_exact_layout(oracle_mod, golden):
     """shortint_woppbs_1bit.rs:665-697 (vertical packing and multi-polynomial LUT layout)."""
     lut = oracle_mod.generate_lut(16, 3, 2, lambda v: v)
