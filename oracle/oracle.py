@@ -17,6 +17,8 @@ _SO = os.path.join(_HERE, "build", "liboracle.so")
 PARAMS_SQRD_LVL_1, PARAMS_SQRD_LVL_4, PARAMS_SQRD_LVL_64, PARAMS_SQRD_LVL_256 = 0, 1, 2, 3
 PARAMS_WOPPBS_8BIT = 4  # shortint_woppbs_8bit.rs:39-86
 PARAMS_SHORTINT_1BIT = 5  # shortint_1bit.rs:62-83
+# blind-rotation transform of a server key built from raw arrays (tfhe_oracle.h or_server_key_from_raw_t)
+TRANSFORMS = {"product": 0, "radix": 1}
 
 
 def build() -> str:
@@ -55,6 +57,8 @@ def lib():
                                   C.POINTER(C.POINTER(_ServerKey))]
         L.or_server_key_from_raw.argtypes = [C.c_int, u64p, u64p, u64p]
         L.or_server_key_from_raw.restype = C.POINTER(_ServerKey)
+        L.or_server_key_from_raw_t.argtypes = [C.c_int, u64p, u64p, u64p, C.c_int]
+        L.or_server_key_from_raw_t.restype = C.POINTER(_ServerKey)
         L.or_client_key_free.argtypes = [C.c_void_p]
         L.or_server_key_free.argtypes = [C.c_void_p]
         for f in ("or_ksk_len", "or_bsk_len", "or_pfpksk_len"):
@@ -154,7 +158,9 @@ def params(pid: int) -> dict:
 class Keys:
     """Client + server key pair generated by the oracle's keygen (same spec as the product)."""
 
-    def __init__(self, pid: int, seed: bytes, threads: int = 8, raw=None):
+    def __init__(self, pid: int, seed: bytes, threads: int = 8, raw=None, transform: str = "product"):
+        """transform (raw keys only): "product" = the blind rotation the product runs (the fused-twiddle
+        transforms for params_sqrd_lvl_64 and the 8-bit set), "radix" = the tfhe-fft-shaped radix schedule."""
         L = lib()
         self.pid = pid
         self.p = params(pid)
@@ -165,7 +171,7 @@ class Keys:
             assert L.or_gen_keys(pid, seed, threads, C.byref(self._ck), C.byref(self._sk)) == 0
         else:
             ksk, bsk, pfpksk = (np.ascontiguousarray(x, dtype=np.uint64) for x in raw)
-            self._sk = L.or_server_key_from_raw(pid, _p64(ksk), _p64(bsk), _p64(pfpksk))
+            self._sk = L.or_server_key_from_raw_t(pid, _p64(ksk), _p64(bsk), _p64(pfpksk), TRANSFORMS[transform])
             self._ck = None
 
     def __del__(self):

@@ -1005,7 +1005,9 @@ static int lf_set(const or_params *p) { return p->N == 512 && p->k == 4 && p->pb
  * model's set) */
 static int lf1k_set(const or_params *p) { return p->N == 1024 && p->k == 2 && p->pbs_l == 6 && p->pbs_b == 7; }
 
-static void server_key_fourier(or_server_key *sk) {
+/* transform: OR_TRANSFORM_PRODUCT (the fused-twiddle transform for the sets above, as the product) or
+ * OR_TRANSFORM_RADIX (the radix-16 / radix-8 schedule shaped like tfhe-fft for every set, no rescale) */
+static void server_key_fourier(or_server_key *sk, int transform) {
     const or_params *p = &sk->p;
     int M = p->N / 2;
     size_t polys = (size_t)p->n * p->pbs_l * (p->k + 1) * (p->k + 1);
@@ -1013,8 +1015,8 @@ static void server_key_fourier(or_server_key *sk) {
     for (size_t i = 0; i < polys; i++)
         or_fft_fwd_torus(sk->fft, sk->bsk + i * p->N, sk->bsk_f + i * M);
     sk->lf = NULL;
-    if (lf_set(p)) sk->lf = or_lf_plan_new();
-    if (lf1k_set(p)) sk->lf = or_lf1k_plan_new();
+    if (transform == OR_TRANSFORM_PRODUCT && lf_set(p)) sk->lf = or_lf_plan_new();
+    if (transform == OR_TRANSFORM_PRODUCT && lf1k_set(p)) sk->lf = or_lf1k_plan_new();
     if (sk->lf) lf_rescale(sk->lf, sk->bsk_f, polys);
 }
 
@@ -1051,7 +1053,7 @@ int or_gen_keys(int param_id, const uint8_t seed[32], int threads, or_client_key
     for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
     free(th);
     free(jobs);
-    server_key_fourier(sk);
+    server_key_fourier(sk, OR_TRANSFORM_PRODUCT);
     *ckp = ck;
     *skp = sk;
     return 0;
@@ -1059,6 +1061,11 @@ int or_gen_keys(int param_id, const uint8_t seed[32], int threads, or_client_key
 
 or_server_key *or_server_key_from_raw(int param_id, const uint64_t *ksk, const uint64_t *bsk,
                                       const uint64_t *pfpksk) {
+    return or_server_key_from_raw_t(param_id, ksk, bsk, pfpksk, OR_TRANSFORM_PRODUCT);
+}
+
+or_server_key *or_server_key_from_raw_t(int param_id, const uint64_t *ksk, const uint64_t *bsk,
+                                        const uint64_t *pfpksk, int transform) {
     or_params p;
     if (or_params_get(param_id, &p)) return NULL;
     or_server_key *sk = (or_server_key *)calloc(1, sizeof(*sk));
@@ -1070,7 +1077,7 @@ or_server_key *or_server_key_from_raw(int param_id, const uint64_t *ksk, const u
     memcpy(sk->ksk, ksk, sizeof(uint64_t) * or_ksk_len(&p));
     memcpy(sk->bsk, bsk, sizeof(uint64_t) * or_bsk_len(&p));
     memcpy(sk->pfpksk, pfpksk, sizeof(uint64_t) * or_pfpksk_len(&p));
-    server_key_fourier(sk);
+    server_key_fourier(sk, transform);
     return sk;
 }
 

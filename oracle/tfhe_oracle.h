@@ -127,6 +127,15 @@ int or_gen_keys(int param_id, const uint8_t seed[32], int threads, or_client_key
 /* Build a server key from raw standard-domain arrays (copied). */
 or_server_key *or_server_key_from_raw(int param_id, const uint64_t *ksk, const uint64_t *bsk,
                                       const uint64_t *pfpksk);
+/* The same with an explicit blind-rotation transform: OR_TRANSFORM_PRODUCT = what the product runs (the
+ * fused-twiddle transforms for params_sqrd_lvl_64 and the 8-bit set, the radix schedule otherwise);
+ * OR_TRANSFORM_RADIX = the radix-16 / radix-8 schedule shaped like tfhe-fft for every set (no conj(E2)
+ * rescale of the Fourier BSK): the PBS-level tie of the fused transforms back to tfhe-fft's
+ * (tests/test_oracle_transforms.py). */
+#define OR_TRANSFORM_PRODUCT 0
+#define OR_TRANSFORM_RADIX 1
+or_server_key *or_server_key_from_raw_t(int param_id, const uint64_t *ksk, const uint64_t *bsk,
+                                        const uint64_t *pfpksk, int transform);
 void or_client_key_free(or_client_key *ck);
 void or_server_key_free(or_server_key *sk);
 size_t or_ksk_len(const or_params *p);
