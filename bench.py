@@ -33,7 +33,7 @@ HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (= FP64 matrix) dense peak, spec
 SPEC_CLOCK_GHZ = 2.4      # the clock the spec peaks assume
 FP64_SUSTAINED_TFLOPS = 58.0  # measured sustained v_fma_f64 rate, all CUs (scripts/probes/fp64_peak.hip)
-PBS_KERNELS = {"1bit": "tae::br512x4::br_kernel<3, true, 12>", "8bit": "tae::br1024::br_kernel<6, true, 7>"}
+PBS_KERNELS = {"1bit": "tae::br512x4::br_kernel<3, true, 12>", "8bit": "tae::br1024::br_kernel<6, true, 7, 2, 1>"}
 
 
 def pbs_algorithmic(p, bits):
@@ -72,6 +72,11 @@ def main():
                          "(--model8-blocks blocks, one step) and report it beside the headline line; auto = on "
                          "at world size 1")
     ap.add_argument("--model8-blocks", type=int, default=64)
+    ap.add_argument("--force-dist", action="store_true",
+                    help="take the torch.distributed branch even at world size 1 (backend nccl = RCCL unless "
+                         "TAE_BENCH_BACKEND says otherwise): communicator init, the device broadcast of the server "
+                         "keys and the round key, device-built contexts, max/min over ranks; launch it under "
+                         "torch.distributed.run (MASTER_ADDR / MASTER_PORT)")
     ap.add_argument("--host-buffers", choices=["auto", "on", "off"], default="auto",
                     help="one extra step with host arrays (PCIe-inclusive rate); auto = on at world 1")
     args = ap.parse_args()
@@ -91,7 +96,8 @@ def main():
     dev = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     torch.cuda.set_device(dev)
     dist = None
-    if world > 1:
+    use_dist = world > 1 or args.force_dist
+    if use_dist:
         import torch.distributed as dist
         if backend == "gloo":
             dist.init_process_group("gloo")
@@ -112,7 +118,8 @@ def main():
     keygen_s = time.time() - t
     ck = tfhe_aes.client_key_from_seed(pid, SEED)
     t = time.time()
-    if world == 1:
+    dist_info = None
+    if not dist:
         ctx = tfhe_aes.context_from_raw(pid, raw, device=dev)
     else:
         from tfhe_aes import _native as N
@@ -120,8 +127,11 @@ def main():
         N.check(N.lib().tae_server_key_sizes(pid, *[C.byref(x) for x in lens]))
         bufs = D.broadcast_u64(dist, raw if rank == 0 else None, [x.value for x in lens], rank, f"cuda:{dev}")
         torch.cuda.synchronize()
+        bcast_s = time.time() - t
         ctx = tfhe_aes.context_from_raw(pid, [b.data_ptr() for b in bufs], device=dev, mem=1)
         ctx._keepalive = bufs
+        dist_info = {"backend": dist.get_backend(), "world": world, "server_key_bytes": int(sum(b.numel() * 8 for b in bufs)),
+                     "server_key_broadcast_s": bcast_s, "key_tensors_on": str(bufs[0].device)}
     key_setup_s = time.time() - t
 
     # ---- expanded key: FHE key schedule on rank 0 (timed separately), broadcast ----
@@ -142,7 +152,7 @@ def main():
         rk_dev = torch.from_numpy(rk_np.view(np.int64)).to(f"cuda:{dev}")
     else:
         rk_dev = torch.empty((44 * 32, L), dtype=torch.int64, device=f"cuda:{dev}")
-    if world > 1:
+    if dist:
         dist.broadcast(rk_dev, src=0)
 
     # ---- this rank's counter blocks (main.rs:108-115), encrypted client side, resident in HBM ----
@@ -156,8 +166,8 @@ def main():
     out_dev = torch.empty_like(blk_dev)
     torch.cuda.synchronize()
 
-    def step():
-        E.encrypt_blocks_device(ctx, rk_dev.data_ptr(), blk_dev.data_ptr(), nb, args.rounds, out_dev.data_ptr())
+    def step(o=out_dev):
+        E.encrypt_blocks_device(ctx, rk_dev.data_ptr(), blk_dev.data_ptr(), nb, args.rounds, o.data_ptr())
 
     for _ in range(args.warmup):
         step()
@@ -180,17 +190,22 @@ def main():
     ctx.set_timing(False)
     if dist:
         elapsed = D.max_over_ranks(dist, elapsed, f"cuda:{dev}")
+    # the timed steps' own output, copied out before anything else writes a ciphertext buffer
+    out = out_dev.cpu().numpy().view(np.uint64)
     # effective shader clock of the PBS launches: one more step, right after the timed ones (chip warm),
-    # with in-kernel clock stamps (a diagnostic mode: each stamped launch is read back synchronously)
+    # with in-kernel clock stamps (a diagnostic mode: each stamped launch is read back synchronously), into
+    # its own output buffer; its ciphertexts must equal the timed steps' bit for bit
+    clk_out = torch.empty_like(out_dev)
     ctx.set_timing(True, clock=True)
-    step()
+    step(clk_out)
     ctx.synchronize()
     clk = ctx.last_stage_times()
     ctx.set_timing(False)
     clock_ghz = clk.get("pbs_clock_ghz")
+    clock_step_identical = bool(np.array_equal(clk_out.cpu().numpy().view(np.uint64), out))
+    del clk_out
 
-    # ---- correctness gate: decrypt and compare with plain AES (outside the timed region) ----
-    out = out_dev.cpu().numpy().view(np.uint64)
+    # ---- correctness gate on the timed steps' output: decrypt and compare with plain AES ----
     got = aes_128.bits_to_blocks(ck.decrypt_bits_raw(out))
     ek_plain = aes_128.key_schedule_plain(README_KEY)
     ok = int(all(g == aes_128.encrypt_block_plain(ek_plain, b, args.rounds) for g, b in zip(got, blocks)))
@@ -289,7 +304,7 @@ def main():
                 "sustained": {"peak": FP64_SUSTAINED_TFLOPS, "frac": (tflops / FP64_SUSTAINED_TFLOPS) if tflops else None,
                               "note": "v_fma_f64 rate the chip holds with every CU busy "
                                       "(scripts/probes/fp64_peak.hip); the spec peak assumes 2.4 GHz"},
-                "effective_clock_ghz": clock_ghz,
+                "effective_clock_ghz": clock_ghz, "clock_step_identical": clock_step_identical,
                 "at_clock": at_clock(tflops, clock_ghz)}
     stage_share = {k: v / args.steps for k, v in stage_ms.items() if k not in ("pbs_launches", "pbs_main_cts")}
 
@@ -318,7 +333,7 @@ def main():
                "stage_ms_per_step": stage_share, "per_sbox_ms": ms_per_step / (nb * 16 * args.rounds),
                "keygen_s": keygen_s, "key_setup_s": key_setup_s, "key_expansion_s": key_expansion_s,
                "encrypt_s": encrypt_s, "correct": bool(ok), "single_block": single, "host_buffers": host_io,
-               "model8": model8}
+               "model8": model8, "dist": dist_info}
         print(json.dumps(rec), flush=True)
     if dist:
         dist.destroy_process_group()
@@ -402,28 +417,35 @@ def model8_leg(torch, dev, nb, threads, steps=3):
     blk_dev = torch.from_numpy(cts.view(np.int64)).to(f"cuda:{dev}")
     out_dev = torch.empty_like(blk_dev)
     torch.cuda.synchronize()
-    step = lambda: E8.encrypt_blocks_device(ctx, rk_dev.data_ptr(), blk_dev.data_ptr(), nb, 10, out_dev.data_ptr())
-    step()
+    step = lambda o: E8.encrypt_blocks_device(ctx, rk_dev.data_ptr(), blk_dev.data_ptr(), nb, 10, o.data_ptr())
+    step(out_dev)
     ctx.synchronize()
-    times = []
+    times, acc = [], {}
+    ctx.set_timing(True)  # HIP events around each stage on the engine stream (no host round trips)
     for _ in range(steps):
         t0 = time.time()
-        step()
+        step(out_dev)
         ctx.synchronize()
         times.append(time.time() - t0)
-    dt = sum(times) / len(times)
-    ctx.set_timing(True, clock=True)  # one more step outside the timed ones: where the time goes
-    step()
-    ctx.synchronize()
-    st = ctx.last_stage_times()
-    clock_ghz = st.get("pbs_clock_ghz")
-    stages = {k: (round(v, 1) if isinstance(v, float) else v) for k, v in st.items()
-              if k not in ("pbs_main", "pbs_main_cts", "pbs_clock_ghz", "pbs_clock_launches")}
+        for kk, v in ctx.last_stage_times().items():
+            acc[kk] = acc.get(kk, 0) + v
     ctx.set_timing(False)
-    got = aes_128.bits_to_blocks(ck.decrypt_bits_raw(out_dev.cpu().numpy().view(np.uint64)))
+    dt = sum(times) / len(times)
+    out = out_dev.cpu().numpy().view(np.uint64)  # the timed steps' output, gated below
+    # one more step with in-kernel clock stamps into its own buffer: the effective clock only
+    clk_out = torch.empty_like(out_dev)
+    ctx.set_timing(True, clock=True)
+    step(clk_out)
+    ctx.synchronize()
+    clock_ghz = ctx.last_stage_times().get("pbs_clock_ghz")
+    ctx.set_timing(False)
+    clock_step_identical = bool(np.array_equal(clk_out.cpu().numpy().view(np.uint64), out))
+    stages = {k: (round(v / steps, 1) if isinstance(v, float) else v // steps) for k, v in acc.items()
+              if k not in ("pbs_main", "pbs_main_cts", "pbs_clock_ghz", "pbs_clock_launches")}
+    got = aes_128.bits_to_blocks(ck.decrypt_bits_raw(out))
     ek_plain = aes_128.key_schedule_plain(README_KEY)
     correct = all(g == aes_128.encrypt_block_plain(ek_plain, b, 10) for g, b in zip(got, blocks))
-    del ctx
+    del ctx, clk_out
     # the circuit bootstrap's PBS launches (one per CBS level and round, nb x 16 x 8 bits each): the
     # dominant kernel of this model, against the same FP64 spec as the headline line
     _, flop_launch = pbs_algorithmic(tfhe_aes.get_params(pid), nb * 16 * 8)
@@ -435,8 +457,9 @@ def model8_leg(torch, dev, nb, threads, steps=3):
                     "algorithmic_flop_per_launch": flop_launch,
                     "avg_launch_ms": pbs_ms / launches if launches else None,
                     "effective_clock_ghz": clock_ghz, "at_clock": at_clock(tf, clock_ghz),
-                    "note": "stage time of the timing step over its PBS launches (HIP events on the engine stream; "
-                            "that step also carries the clock stamps)"}
+                    "clock_step_identical": clock_step_identical,
+                    "note": "stage time per timed step over its PBS launches (HIP events on the engine stream); the "
+                            "clock comes from one extra stamped step"}
     return {"config": f"ShortintWoppbs8BitSboxPbsAesEncrypt, {nb} counter blocks x 10 rounds on 1 GPU "
                       f"(BASELINE configs[4]); 1 warm-up + {steps} timed steps", "blocks": nb, "s_per_step": dt,
             "s_per_step_each": times, "spread": (max(times) - min(times)) / dt,

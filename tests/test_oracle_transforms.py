@@ -25,7 +25,6 @@ from concurrent.futures import ThreadPoolExecutor
 import numpy as np
 import pytest
 
-from tests.conftest import SEED
 from tfhe_aes import aes_128
 
 MASK = (1 << 64) - 1

@@ -226,7 +226,8 @@ class Engine {
     void (*br1024lat_)(const uint64_t *, int, const uint64_t *, const cplx *, uint64_t *, long, uint64_t, uint64_t,
                        const cplx *, const double *) = nullptr;
     size_t br1024lat_lds_ = 0;
-    bool x4_512_ = false;     // N = 512, k = 4 (lvl_64): batched blind rotations br512x4 / br512lat
+    bool x4_512_ = false;     // PBS N = 512, k = 4, 3 x 2^12 (lvl_64): br512x4 / br512lat on the fused transform
+    bool x4_vp_ = false;      // ... and cbs 1 x 2^13: vertical packing on br512x4<1, false, 13>
     long lat_max_ = 256;      // batch size up to which br512lat runs (TAE_BR_LAT_MAX)
     int num_cu_ = 256;
     double *d_lf_ = nullptr;  // the fused-twiddle transform's table (lf512.hpp: params_sqrd_lvl_64, lf1k.hpp: 8-bit)

@@ -743,7 +743,10 @@ void Engine::init_common() {
     // batched N=512, k=4 blind rotation (params_sqrd_lvl_64): br512x4 for large batches, br512lat for
     // small ones.  TAE_BR_LAT_MAX (a tuning knob, both sides pinned by tests) is the batch size up
     // to which br512lat runs (0: never).
-    x4_512_ = p_.N == 512 && p_.k == 4 && p_.pbs_l == 3 && p_.pbs_b == 12 && p_.cbs_l == 1 && p_.cbs_b == 13;
+    // The PBS shape alone decides the fused transform and its conj(E2)-rescaled BSK, exactly as the oracle's
+    // lf_set (tfhe_oracle.c); the vertical-packing instantiation br512x4<1, false, 13> also needs cbs 1 x 2^13.
+    x4_512_ = p_.N == 512 && p_.k == 4 && p_.pbs_l == 3 && p_.pbs_b == 12;
+    x4_vp_ = x4_512_ && p_.cbs_l == 1 && p_.cbs_b == 13;
     // the 8-bit model's set: its PBS blind rotations run the N = 1024 fused-twiddle transform (lf1k.hpp)
     lf1k_ = p_.N == 1024 && p_.k == 2 && p_.pbs_l == 6 && p_.pbs_b == 7;
     if (x4_512_ || lf1k_) {  // the blind rotations' fused-twiddle transform (lf512.hpp / lf1k.hpp)
@@ -759,9 +762,10 @@ void Engine::init_common() {
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)br512lat::lds_bytes(3)));
         HIPC(hipFuncSetAttribute((const void *)br512x4::br_kernel<3, true, 12>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    }
+    if (x4_vp_)
         HIPC(hipFuncSetAttribute((const void *)br512x4::br_kernel<1, false, 13>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    }
     // batched N=1024, k=2 blind rotation (br1024.hpp); other shapes run the generic kernels
     if (p_.N == 1024 && p_.k == 2) {
         br1024_pbs_ = br1024::pick<2>(true, p_.pbs_l, p_.pbs_b);
@@ -1184,7 +1188,7 @@ void Engine::vertical_packing(const cplx *d_ggsw_f, size_t G, int n_in, const ui
         vertical_packing_tree(d_ggsw_f, G, n_in, n_in - logN, d_lut, n_out, d_out);
         return;
     }
-    if (x4_512_) {
+    if (x4_vp_) {
         const size_t wgs = G * (size_t)((n_out + kBrC - 1) / kBrC);
         br512x4::br_kernel<1, false, 13><<<(unsigned)wgs, br512x4::THREADS, br512x4::lds_bytes(), stream_>>>(
             nullptr, 0, d_lut, n_out, d_ggsw_f, n_in, d_out, (long)G, 0, 0, d_twist_, d_w_, nullptr, nullptr);
