@@ -167,26 +167,25 @@ def test_context_shared_across_host_threads(gpu_context, client):
 
 def test_timing_modes_bit_identical(gpu_context, client):
     """tae_set_timing: mode 1 (HIP events per stage) and mode 2 (plus the in-kernel clock stamps of the
-    throughput blind rotation, bench.py's effective_clock_ghz) leave the ciphertexts of a br512x4 PBS batch
+    throughput blind rotation, bench.py's effective_clock_ghz) leave the ciphertexts of a batched call
     bit-identical to mode 0; mode 2 fills the clock fields with a plausible shader clock; mode 3 is
-    TAE_E_ARG (before this mode existed any nonzero value meant "on")."""
-    B = 3 * 256 * 2  # two whole br512x4 rounds, no br512lat remainder
-    bits = np.random.default_rng(11).integers(0, 2, size=B).astype(np.uint8)
-    cts = client.encrypt_bits_raw(bits, start_index=7_000_000)
-    small = np.zeros((B, 678), dtype=np.uint64)
-    N.check(N.lib().tae_stage_keyswitch(gpu_context._h, _vp(cts), B, _vp(small), N.TAE_MEM_HOST))
+    TAE_E_ARG (before mode 2 existed any nonzero value meant "on").  8 blocks x 1 round: one SubBytes
+    circuit bootstrap of 1024 bits = one br512x4 launch of 768 + a br512lat remainder of 256."""
+    E = aes_128.ShortintWoppbs1BitSboxGalMulPbsAesEncrypt
+    rk = client.encrypt_bits_raw([(i * 5 + 1) >> 1 & 1 for i in range(1408)], start_index=7_000_000)
+    nb = 8
+    bits = [(i * 29 + 7) >> 3 & 1 for i in range(128 * nb)]
+    blocks = client.encrypt_bits_raw(bits, start_index=7_100_000).reshape(nb, 128, BIG)
     outs = {}
     try:
         for mode in (0, 1, 2):
             N.check(N.lib().tae_set_timing(gpu_context._h, mode))
-            out = np.zeros((B, BIG), dtype=np.uint64)
-            N.check(N.lib().tae_stage_pbs_shift_boolean(gpu_context._h, _vp(small), B, 1, _vp(out), N.TAE_MEM_HOST))
-            outs[mode] = (out, gpu_context.last_stage_times())
+            outs[mode] = (E.encrypt_blocks_raw(gpu_context, rk, blocks, 1), gpu_context.last_stage_times())
     finally:
         N.check(N.lib().tae_set_timing(gpu_context._h, 0))
     assert np.array_equal(outs[1][0], outs[0][0]) and np.array_equal(outs[2][0], outs[0][0])
     t1, t2 = outs[1][1], outs[2][1]
-    assert t1["pbs_main"] > 0 and t1["pbs_main_cts"] == B and "pbs_clock_ghz" not in t1
+    assert t1["pbs"] > 0 and t1["pbs_main"] > 0 and t1["pbs_main_cts"] == 768 and "pbs_clock_ghz" not in t1, t1
     assert t2["pbs_clock_launches"] >= 1 and 1.0 < t2["pbs_clock_ghz"] < 3.0, t2
     assert N.lib().tae_set_timing(gpu_context._h, 3) == N.TAE_E_ARG
     assert N.lib().tae_set_timing(gpu_context._h, -1) == N.TAE_E_ARG
