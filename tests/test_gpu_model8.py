@@ -58,15 +58,15 @@ def test_pbs_shift_boolean8_bit_exact(gpu_context8, oracle_keys8, client8, level
         assert min(err, (1 << 64) - err) < 1 << (63 - 6 * level), (i, level)  # within alpha
 
 
-@pytest.mark.parametrize("lat,pair,B", [("1", "1", 5), ("0", "1", 5), ("0", "0", 5), ("1", "1", 300),
-                                        ("1", "1", 513)])
-def test_pbs8_kernel_variants_bit_exact(product_raw8, oracle_keys8, client8, lat, pair, B):
+@pytest.mark.parametrize("lat,pair,B,occ2", [("1", "1", 5, "0"), ("0", "1", 5, "0"), ("0", "0", 5, "0"),
+                                             ("1", "1", 300, "0"), ("1", "1", 513, "0"), ("1", "1", 513, "1")])
+def test_pbs8_kernel_variants_bit_exact(product_raw8, oracle_keys8, client8, lat, pair, B, occ2):
     """The N=1024 blind-rotation variants the engine picks, all on the fused-twiddle transform (lf1k.hpp,
     the oracle's or_lf1k_*): for batches up to one ciphertext per CU the 1024-thread latency kernel
     (br1024lat, default), or with TAE_B1K_LAT=0 br1024 with one ciphertext per workgroup and two levels
     per pass (or one: TAE_B1K_PAIR=0); and two ciphertexts per workgroup (B > the CU count, odd tail
-    workgroup of one)."""
-    env = {"TAE_B1K_LAT": lat, "TAE_B1K_PAIR": pair}
+    workgroup of one); TAE_B1K_OCC2=1: large batches as one ciphertext per workgroup, two per CU."""
+    env = {"TAE_B1K_LAT": lat, "TAE_B1K_PAIR": pair, "TAE_B1K_OCC2": occ2}
     os.environ.update(env)
     try:
         ctx = tfhe_aes.context_from_raw(tfhe_aes.PARAMS_WOPPBS_8BIT, product_raw8[1], device=0)

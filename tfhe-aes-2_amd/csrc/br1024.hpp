@@ -110,8 +110,12 @@ __device__ __forceinline__ void dft8(cplx *v, cplx w1, cplx w3) {
 // C = 1 and an even level count, LP = 2 runs the FFTs of two decomposition levels together (6 jobs on
 // 8 waves instead of 3), halving the level passes and their barriers; the MAC still consumes the
 // levels in descending order.
-template <int LEV, bool PBS, int BLOG, int C, int LP>
-__global__ void __launch_bounds__(THREADS, 1)
+// (HIP: the second launch bound is the minimum waves per SIMD.)
+// OCC workgroups per CU: 1 (two waves per SIMD, 256 VGPRs) or 2 (C = 1 workgroups, four waves per SIMD,
+// <= 128 VGPRs: the lane's fused-DFT8 constants and twiddles read from LDS at each use; the two workgroups'
+// barriers are independent, so one's MAC can run beside the other's FFTs).
+template <int LEV, bool PBS, int BLOG, int C, int LP, int OCC = 1>
+__global__ void __launch_bounds__(THREADS, 2 * OCC)
     br_kernel(const uint64_t *__restrict__ lwe_in, int n, const uint64_t *__restrict__ lut, int n_out,
               const cplx *__restrict__ ggsw_base, int n_in, uint64_t *__restrict__ out, long B,
               uint64_t body_add, uint64_t out_add, const cplx *__restrict__ twist, const cplx *__restrict__ untwist,
@@ -195,7 +199,7 @@ __global__ void __launch_bounds__(THREADS, 1)
     // register budget (two waves per SIMD) holds them, which saves 14 LDS reads per FFT job: the CBS
     // launch (C = 2, 2048 ciphertexts) takes 64.1 ms instead of 70.9, same box. The LP = 2 variant
     // would spill.
-    constexpr bool WREG = LP == 1;
+    constexpr bool WREG = LP == 1 && OCC == 1;
     cplx w0r[7], w1r[7];
     // LFT: likewise the lane's fused-DFT8 constants of the forward passes 1 / 2 and the inverse passes
     // 1 / 0, and the lane-uniform ones of pass 0
@@ -292,16 +296,22 @@ __global__ void __launch_bounds__(THREADS, 1)
 
         BPROF(0);
         for (int lev0 = LEV; lev0 >= 1; lev0 -= LP) {
+            // the level's GGSW values at this thread's Fourier position: before the FFTs (their L2 latency
+            // hidden behind them), or with OCC = 2 after the barrier (the register budget; the other
+            // workgroup of the CU runs meanwhile)
+            auto load_gv = [&] {
 #pragma unroll
-            for (int lh = 0; lh < LP; lh++)
+                for (int lh = 0; lh < LP; lh++)
 #pragma unroll
-                for (int p = 0; p < K1; p++)
+                    for (int p = 0; p < K1; p++)
 #pragma unroll
-                    for (int q = 0; q < K1; q++) {
-                        const int soff = gstep + (((lev0 - lh - 1) * K1 + p) * K1 + q) * M * (int)sizeof(cplx);
-                        const u32x4 rv = __builtin_amdgcn_raw_buffer_load_b128(grs, gvoff, soff, 0);
-                        __builtin_memcpy(&gv[(lh * K1 + p) * K1 + q], &rv, sizeof(cplx));
-                    }
+                        for (int q = 0; q < K1; q++) {
+                            const int soff = gstep + (((lev0 - lh - 1) * K1 + p) * K1 + q) * M * (int)sizeof(cplx);
+                            const u32x4 rv = __builtin_amdgcn_raw_buffer_load_b128(grs, gvoff, soff, 0);
+                            __builtin_memcpy(&gv[(lh * K1 + p) * K1 + q], &rv, sizeof(cplx));
+                        }
+            };
+            if constexpr (OCC == 1) load_gv();
             const int lev = lev0 - jlh;  // this wave's level
             if (fjob) {
                 cplx *X = buf + jb * BUF_STRIDE;
@@ -397,6 +407,7 @@ __global__ void __launch_bounds__(THREADS, 1)
             br512::lds_sync();
             BPROF(2);
             s_setprio_c<3>();
+            if constexpr (OCC == 2) load_gv();
             // MAC at Fourier position pos: accumulator (q, c) = accr[q * C + c]; levels descending, p ascending
 #pragma unroll
             for (int lp = 0; lp < LP * K1; lp++) {
@@ -538,6 +549,12 @@ inline size_t lds_bytes(int C, int LP = 1, bool lft = false) {
 // (levels, base_log) combinations of the N=1024 parameter sets: returns the kernel or nullptr
 typedef void (*kernel_t)(const uint64_t *, int, const uint64_t *, int, const cplx *, int, uint64_t *, long, uint64_t,
                          uint64_t, const cplx *, const cplx *, const cplx *, const double *, uint64_t *);
+// the 8-bit model's PBS as one ciphertext per workgroup at two workgroups per CU (OCC = 2)
+inline kernel_t pick_occ2(int levels, int base_log) {
+    if (levels == 6 && base_log == 7) return (kernel_t)br_kernel<6, true, 7, 1, 1, 2>;
+    return nullptr;
+}
+
 // LP levels per pass; LP = 2 only for the PBS with at least two passes (nullptr otherwise)
 template <int C, int LP = 1>
 inline kernel_t pick(bool pbs, int levels, int base_log) {

@@ -220,6 +220,7 @@ class Engine {
                         uint64_t, const cplx *, const cplx *, const cplx *, const double *, uint64_t *) = nullptr;
     decltype(br1024_pbs_) br1024_vp_ = nullptr;
     decltype(br1024_pbs_) br1024_pbs1_ = nullptr;  // one ciphertext per workgroup (small batches)
+    decltype(br1024_pbs_) br1024_occ2_ = nullptr;  // A/B: one per workgroup, two workgroups per CU
     int br1024_pbs1_lp_ = 1;                       // its levels per pass
     bool lf1k_ = false;                            // the 8-bit model's PBS: the N = 1024 fused transform (lf1k.hpp)
     // latency blind rotation, one ciphertext per 1024-thread workgroup (br1024lat.hpp), or nullptr

@@ -778,6 +778,14 @@ void Engine::init_common() {
             br1024_pbs1_ = br1024::pick<1>(true, p_.pbs_l, p_.pbs_b);
         }
         br1024_vp_ = br1024::pick<2>(false, p_.cbs_l, p_.cbs_b);
+        // TAE_B1K_OCC2=1 (A/B knob): large PBS batches as one ciphertext per workgroup, two per CU
+        const char *occ2 = getenv("TAE_B1K_OCC2");
+        if (occ2 && occ2[0] == '1' && lf1k_) {
+            br1024_occ2_ = br1024::pick_occ2(p_.pbs_l, p_.pbs_b);
+            if (br1024_occ2_)
+                HIPC(hipFuncSetAttribute((const void *)br1024_occ2_, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)br1024::lds_bytes(1, 1, true)));
+        }
         for (auto kf : {br1024_pbs_, br1024_vp_})
             if (kf)
                 HIPC(hipFuncSetAttribute((const void *)kf, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1030,6 +1038,15 @@ void Engine::bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint
         br1024lat_<<<(unsigned)B, br1024lat::THREADS, br1024lat_lds_, stream_>>>(
             d_small, p_.n, d_lut_glwe, d_bsk_f_, d_big, (long)B, body_add, out_add, d_w_, d_lf_);
         HIPC(hipGetLastError());
+        return;
+    }
+    if (br1024_occ2_ && (long)B > (long)num_cu_) {
+        uint64_t *clk = clock_buffer(B);
+        br1024_occ2_<<<(unsigned)B, br1024::THREADS, br1024::lds_bytes(1, 1, true), stream_>>>(
+            d_small, p_.n, d_lut_glwe, 0, d_bsk_f_, 0, d_big, (long)B, body_add, out_add, d_twist_, d_untwist_, d_w_,
+            d_lf_, clk);
+        HIPC(hipGetLastError());
+        record_clock(clk, B);
         return;
     }
     if (br1024_pbs_) {
