@@ -385,7 +385,11 @@ __global__ void __launch_bounds__(THREADS, 1)
             }
             }
             PROF_T(2);
+#ifdef TAE_X4_NOBARF  // timing-only bound (garbage): no barrier between the FFTs and the MAC
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
             lds_sync();
+#endif
             PROF_T(3);
             PRIO(3);
             switch (grp) {
@@ -395,7 +399,11 @@ __global__ void __launch_bounds__(THREADS, 1)
             default: mac_level<3>(buf, spos, accr, gv); break;
             }
             PROF_T(4);
+#ifdef TAE_X4_NOBARM  // timing-only bound (garbage): no barrier between a level's MAC and the next level's pass A
+            if (lev == 1) lds_sync();
+#else
             lds_sync();
+#endif
             PROF_T(5);
             PRIO(3);
         }
