@@ -517,9 +517,13 @@ __global__ void __launch_bounds__(256 * WM, 1)
     for (int ks = 0; ks < nk; ks++) {
         wait_steps(min(G4S - 2, nk - 1 - ks));
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#ifndef TAE_G6_NOBAR  // timing-only bound (racy): no per-step barrier
         __builtin_amdgcn_s_barrier();
+#endif
         __builtin_amdgcn_sched_barrier(0);
+#ifndef TAE_G6_NODMA  // timing-only bound (stale tiles): no operand stream after the prologue
         if (ks + G4S - 1 < nk) stage((ks + G4S - 1) % G4S, ks + G4S - 1);
+#endif
         const int8_t *a_s = smem_g + (ks % G4S) * SAB, *b_s = a_s + SA;
         v4i fa[2][3], fb[2][2];
 #pragma unroll
