@@ -111,6 +111,24 @@ def test_multivariate_batched_equals_single(s1):
             assert ck.decrypt_bits_raw(out[g, f][None])[0] == tabs[f][v]
 
 
+def test_multivariate_chunks_equal_one_batch(s1, monkeypatch):
+    """s1_multivariate runs independent groups in chunks of a row budget (TAE_S1_ROWS): with a budget of one
+    group per chunk the 4-group call must give the one-batch call's outputs word for word."""
+    ck, _, _ = s1
+    tabs = [[1, 0, 0, 1, 0, 1, 1, 0], [0, 0, 0, 1, 0, 1, 1, 1]]
+    mvs = [S.MultivariateTestVector(3, t) for t in tabs]
+    vals = [0b001, 0b100, 0b111, 0b010]
+    bits = ck.encrypt_bits_raw([(v >> (2 - i)) & 1 for v in vals for i in range(3)], start_index=800).reshape(4, 3, -1)
+    _, keys = tfhe_aes.generate_keys_raw(P5, SEED, threads=16)
+    monkeypatch.setenv("TAE_S1_ROWS", "8")  # 2 functions x 4 vectors: one group per chunk
+    chunked = S.calculate_multivariate_function_raw(tfhe_aes.context_from_raw(P5, keys, device=0), bits, mvs)
+    monkeypatch.setenv("TAE_S1_ROWS", "100000")
+    whole = S.calculate_multivariate_function_raw(tfhe_aes.context_from_raw(P5, keys, device=0), bits, mvs)
+    assert np.array_equal(chunked, whole)
+    for g, v in enumerate(vals):
+        assert [ck.decrypt_bits_raw(whole[g, f][None])[0] for f in range(2)] == [tabs[0][v], tabs[1][v]]
+
+
 def test_aes_one_round_and_key_schedule(s1):
     """Shortint1BitSboxPbsAesEncrypt (fhe_impls/shortint_1bit.rs:52-72) through the fhe_sbox_pbs driver: one
     round (ARK0, SubBytes = 8 selector trees per byte, ShiftRows, ARK(rk10)) decrypts to plain AES; the FHE key

@@ -37,7 +37,7 @@ void hip_check(hipError_t e, const char *what) {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr size_t kS1Rows = 16384;  // shortint_1bit selector trees: level-0 bootstraps per chunk
+constexpr size_t kS1Rows = 16384;  // shortint_1bit selector trees: level-0 bootstraps per chunk (at least)
 
 // ---------------------------------------------------------------------------------------------
 // External product on an LDS-resident GLWE accumulator:
@@ -1474,11 +1474,15 @@ void Engine::s1_multivariate(const uint64_t *d_bits, size_t G, int nbits, const 
     require_s1();
     if (!G) return;
     if (nbits < 1 || nbits > 8) throw std::runtime_error("multivariate functions take 1..8 bits");
-    // groups are independent: run them in chunks whose level-0 batch stays near kS1Rows bootstraps, so the
-    // scratch (~60 KB per row: inputs, outputs, big LWEs, packing keyswitches, test vectors) is bounded
-    // (~1 GB) whatever the batch, and a chunk still fills the chip
+    // groups are independent: run them in chunks of about `rows` level-0 bootstraps, so the scratch (~60 KB
+    // per row: inputs, outputs, big LWEs, packing keyswitches, test vectors) is bounded whatever the batch.
+    // Each selector level halves the batch; at 128 rows per CU the last level of an 8-bit tree still has a
+    // bootstrap per CU (the AES S-box: 8 x 128 rows per group, 32 groups per chunk on 256 CUs, 2 GB).
+    // TAE_S1_ROWS overrides the row budget (tests, A/B).
+    const char *rows_env = getenv("TAE_S1_ROWS");
+    const size_t rows = rows_env ? (size_t)atol(rows_env) : std::max<size_t>(kS1Rows, 128 * (size_t)num_cu_);
     const size_t rows_per_group = (size_t)n_fn << (nbits - 1);
-    const size_t gc = std::max<size_t>(1, kS1Rows / rows_per_group);
+    const size_t gc = std::max<size_t>(1, rows / rows_per_group);
     const size_t L = p_.small_len();
     for (size_t g0 = 0; g0 < G; g0 += gc)
         s1_multivariate_chunk(d_bits + g0 * nbits * L, std::min(gc, G - g0), nbits, d_tvs, n_fn,
