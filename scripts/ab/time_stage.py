@@ -7,6 +7,8 @@ correct libraries are checked by the parity tests, not here):
   pbs1lat  1-bit model PBS stage, B = 128 (one AES block: br512lat)
   pbs8     8-bit model PBS stage, B = TAE_B (default 8192: br1024 C = 2; <= 256: br1024lat)
   pfks1    1-bit model PFKS into GGSW, B = TAE_B (default 16384)
+  vp1      1-bit model vertical packing, 8 -> 24 LUT over TAE_B / 8 groups (default 2048 = 128 blocks), on the
+           Fourier GGSWs of random torus GGSWs
 The time is the minimum over TAE_REPS (default 3) launches after one warm-up; with TAE_CLOCK=1 one more
 launch runs with the in-kernel clock stamps and its effective shader clock is printed beside it.
 """
@@ -24,7 +26,7 @@ from tfhe_aes import _native as N  # noqa: E402
 SEED = bytes(range(32))
 shape = sys.argv[1] if len(sys.argv) > 1 else "pbs1"
 pid = tfhe_aes.PARAMS_WOPPBS_8BIT if shape == "pbs8" else tfhe_aes.PARAMS_SQRD_LVL_64
-default_b = {"pbs1": 16383, "pbs1lat": 128, "pbs8": 8192, "pfks1": 16384}[shape]
+default_b = {"pbs1": 16383, "pbs1lat": 128, "pbs8": 8192, "pfks1": 16384, "vp1": 16384}[shape]
 B = int(os.environ.get("TAE_B", default_b))
 reps = int(os.environ.get("TAE_REPS", "3"))
 p = tfhe_aes.get_params(pid)
@@ -32,7 +34,18 @@ _, keys = tfhe_aes.generate_keys_raw(pid, SEED, threads=16)
 ctx = tfhe_aes.context_from_raw(pid, keys, device=0)
 del keys
 g = torch.Generator(device="cuda").manual_seed(1)
-if shape == "pfks1":
+if shape == "vp1":
+    G = B // 8
+    glwe = (p["k"] + 1) * p["N"]
+    std = torch.randint(-2**62, 2**62, (B, p["cbs_l"] * (p["k"] + 1) * glwe), dtype=torch.int64, device="cuda", generator=g)
+    gf = torch.empty((B, p["cbs_l"] * (p["k"] + 1) * (p["k"] + 1) * (p["N"] // 2) * 2), dtype=torch.float64, device="cuda")
+    N.check(N.lib().tae_stage_ggsw_fourier(ctx._h, C.c_void_p(std.data_ptr()), B, C.c_void_p(gf.data_ptr()), N.TAE_MEM_DEVICE))
+    del std
+    lut = torch.randint(-2**62, 2**62, (24, p["N"]), dtype=torch.int64, device="cuda", generator=g)
+    dst = torch.empty((G * 24, p["k"] * p["N"] + 1), dtype=torch.int64, device="cuda")
+    call = lambda: N.lib().tae_stage_vertical_packing(ctx._h, C.c_void_p(gf.data_ptr()), G, 8, C.c_void_p(lut.data_ptr()),
+                                                      24, C.c_void_p(dst.data_ptr()), N.TAE_MEM_DEVICE)
+elif shape == "pfks1":
     src = torch.randint(-2**62, 2**62, (B, p["k"] * p["N"] + 1), dtype=torch.int64, device="cuda", generator=g)
     dst = torch.empty((B, p["cbs_l"] * (p["k"] + 1) * (p["k"] + 1) * p["N"]), dtype=torch.int64, device="cuda")
     call = lambda: N.lib().tae_stage_pfks_ggsw(ctx._h, C.c_void_p(src.data_ptr()), B, 1, C.c_void_p(dst.data_ptr()),
@@ -51,7 +64,7 @@ for it in range(reps + 1):
     ctx.synchronize()
     ts.append(time.time() - t)
 ghz = ""
-if os.environ.get("TAE_CLOCK") == "1" and shape != "pfks1":
+if os.environ.get("TAE_CLOCK") == "1" and shape not in ("pfks1", "vp1"):
     ctx.set_timing(True, clock=True)
     N.check(call())
     ctx.synchronize()

@@ -153,9 +153,12 @@ __global__ void __launch_bounds__(THREADS, 2 * OCC)
         ct0 = (long)blockIdx.x * C;
         nct = (int)min((long)C, B - ct0);
     } else {
+        // XCD-aware order (br512x4.hpp): a group's workgroups share one XCD's L2
+        const int nwg = (int)gridDim.x, q8 = nwg >> 3, r8 = nwg & 7, x8 = (int)blockIdx.x & 7;
+        const int lb = x8 * q8 + min(x8, r8) + ((int)blockIdx.x >> 3);
         const int per_group = (n_out + C - 1) / C;
-        g = blockIdx.x / per_group;
-        ct0 = (long)(blockIdx.x - g * per_group) * C;
+        g = lb / per_group;
+        ct0 = (long)(lb - g * per_group) * C;
         nct = min(C, n_out - (int)ct0);
     }
     const bool jvalid = fjob && jct < nct;

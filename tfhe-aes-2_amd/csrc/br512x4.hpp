@@ -177,9 +177,14 @@ __global__ void __launch_bounds__(THREADS, 1)
         ct0 = (long)blockIdx.x * C;
         nct = (int)min((long)C, B - ct0);
     } else {
+        // XCD-aware order: blocks b, b + 8, b + 16, ... run on one XCD, so give each XCD a contiguous range of
+        // the (group, outputs) order: the workgroups of a group then read its GGSWs from one L2 (round 4: 13.3 GB
+        // of L2-miss traffic per launch against 1.7 GB of GGSW, every group's 8 workgroups on 8 XCDs)
+        const int nwg = (int)gridDim.x, q8 = nwg >> 3, r8 = nwg & 7, x8 = (int)blockIdx.x & 7;
+        const int lb = x8 * q8 + min(x8, r8) + ((int)blockIdx.x >> 3);
         const int per_group = (n_out + C - 1) / C;
-        g = blockIdx.x / per_group;
-        ct0 = (long)(blockIdx.x - g * per_group) * C;
+        g = lb / per_group;
+        ct0 = (long)(lb - g * per_group) * C;
         nct = min(C, n_out - (int)ct0);
     }
     const bool jvalid = fjob && jct < nct;
