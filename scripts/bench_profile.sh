@@ -21,6 +21,7 @@ if [ "${PMC:-1}" = "1" ]; then
   timeout -k 10 $T rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 "$ROOT/bench.py" $ARGS > /dev/null 2> "$OUT/pmc_write.err" || { echo "pmc write failed rc=$?"; tail -30 "$OUT/pmc_write.err"; exit 1; }
   timeout -k 10 $T rocprofv3 --pmc TCC_EA0_RDREQ TCC_EA0_RDREQ_DRAM --output-format csv -d "$OUT/pmc_dram" -o run -- python3 "$ROOT/bench.py" $ARGS > /dev/null 2> "$OUT/pmc_dram.err" || { echo "pmc dram failed rc=$?"; tail -30 "$OUT/pmc_dram.err"; }
   timeout -k 10 $T rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY --output-format csv -d "$OUT/pmc_sq" -o run -- python3 "$ROOT/bench.py" $ARGS > /dev/null 2> "$OUT/pmc_sq.err" || { echo "pmc sq failed rc=$?"; tail -30 "$OUT/pmc_sq.err"; }
+  timeout -k 10 $T rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_mfma" -o run -- python3 "$ROOT/bench.py" $ARGS > /dev/null 2> "$OUT/pmc_mfma.err" || { echo "pmc mfma failed rc=$?"; tail -30 "$OUT/pmc_mfma.err"; }
 fi
 python3 "$ROOT/scripts/prof_summary.py" "$OUT" $BLOCKS > "$OUT/prof_summary.txt" 2>&1 || true
 cat "$OUT/prof_summary.txt"

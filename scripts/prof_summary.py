@@ -54,7 +54,7 @@ def main():
             print("  %-44s calls=%-5s avg=%.3f ms  %5.1f%%" % (short(name)[:44], r.get("Calls"), avg / 1e6,
                                                                float(r.get("Percentage") or 0)))
     pmc = {}
-    for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_dram"):
+    for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_dram", "pmc_mfma"):
         path = find(out, sub, "*counter_collection.csv")
         if not path:
             continue
