@@ -37,6 +37,11 @@ void hip_check(hipError_t e, const char *what) {
 namespace {
 
 constexpr int kThreads = 256;
+#ifndef TAE_G6_WM
+constexpr int kG6WM = 4;  // PFKS GEMM: 96 x WM ciphertexts per workgroup tile, 256 x WM threads
+#else
+constexpr int kG6WM = TAE_G6_WM;
+#endif
 constexpr size_t kS1Rows = 16384;  // shortint_1bit selector trees: level-0 bootstraps per chunk (at least)
 
 // ---------------------------------------------------------------------------------------------
@@ -858,8 +863,8 @@ Engine::Engine(const ServerKeyRaw &keys, int device) : p_(keys.p), device_(devic
 void Engine::prepare_mfma_keys() {
     HIPC(hipFuncSetAttribute((const void *)ksgemm::gemm_g6<6, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)ksgemm::gemm_g6_lds<4>()));
-    HIPC(hipFuncSetAttribute((const void *)ksgemm::gemm_g6<6, 4, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)ksgemm::gemm_g6_lds<4>()));
+    HIPC(hipFuncSetAttribute((const void *)ksgemm::gemm_g6<6, kG6WM, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)ksgemm::gemm_g6_lds<kG6WM>()));
     // int8-MFMA keyswitches when the digits fit their limbs (PFKS 17-bit digits as 3 x 6-bit limbs,
     // KS digits as one byte); otherwise (params_sqrd_lvl_1: pfks base 2^24) the u64 VALU kernels
     mfma_ks_ = p_.pfks_b <= 16 && p_.ks_b <= 7;
@@ -1091,8 +1096,9 @@ void Engine::pfks_into_ggsw(const uint64_t *d_big, uint64_t *d_ggsw, size_t B, i
     if (mfma_ks_ && pf_kl_ && (long)B >= pf_kl_min_) {
         // K layout: rows = ciphertexts, K = (K+1) x S limb slots (ksgemm.hpp KSlots)
         const int K = p_.K(), kd = (K + 1) * pf_slots_.S;
-        const long mt = (long)((B + 383) / 384);  // 384-ciphertext tiles
-        ensure_digits(d_digits_, cap_digits_, (size_t)mt * 384, kd, kp_pf_kl_, stream_, true);
+        constexpr long TMR = 96 * kG6WM;  // ciphertexts per tile (384)
+        const long mt = (long)((B + TMR - 1) / TMR);
+        ensure_digits(d_digits_, cap_digits_, (size_t)mt * TMR, kd, kp_pf_kl_, stream_, true);
         const size_t thr = B * (size_t)(K + 1);
         bool clamp = false;
         for (int l = 0; l < p_.pfks_l; l++) clamp = clamp || pf_slots_.clamp[l];
@@ -1108,7 +1114,7 @@ void Engine::pfks_into_ggsw(const uint64_t *d_big, uint64_t *d_ggsw, size_t B, i
         const long out_stride = (long)p_.cbs_l * ncols;
         const long ntiles = ((long)ncols * 8 + ksgemm::BTN - 1) / ksgemm::BTN;
         uint64_t *dst = d_ggsw + (size_t)(level - 1) * ncols;
-        ksgemm::gemm_g6<6, 4, true><<<(unsigned)(mt * ntiles), 1024, ksgemm::gemm_g6_lds<4>(), stream_>>>(
+        ksgemm::gemm_g6<6, kG6WM, true><<<(unsigned)(mt * ntiles), 256 * kG6WM, ksgemm::gemm_g6_lds<kG6WM>(), stream_>>>(
             d_digits_, d_pf_bt_kl_, kp_pf_kl_, mt, ncols, dst, out_stride, (long)B, d_pf_corr_);
         if (clamp) {
             const long pf_blk = (long)(K + 1) * p_.pfks_l * glwe;
