@@ -998,9 +998,10 @@ static void *kg_worker(void *arg) {
     return NULL;
 }
 
-/* the parameter sets whose blind rotation runs the fused-twiddle transform (the product's br512x4 /
- * br512lat shape: N = 512, k = 4, 3 levels of 2^12 = params_sqrd_lvl_64) */
-static int lf_set(const or_params *p) { return p->N == 512 && p->k == 4 && p->pbs_l == 3 && p->pbs_b == 12; }
+/* the parameter sets whose blind rotation runs the fused-twiddle transform: the product's br512x4 /
+ * br512lat shape N = 512, k = 4 (params_sqrd_lvl_64, 3 levels of 2^12, and the shortint_1bit set, 7 levels
+ * of 2^6; the engine's lf512_ tests the same two fields) */
+static int lf_set(const or_params *p) { return p->N == 512 && p->k == 4; }
 /* ... and the N = 1024 one (the product's br1024 / br1024lat PBS shape: k = 2, 6 levels of 2^7, the 8-bit
  * model's set) */
 static int lf1k_set(const or_params *p) { return p->N == 1024 && p->k == 2 && p->pbs_l == 6 && p->pbs_b == 7; }

@@ -150,7 +150,7 @@ __global__ void __launch_bounds__(THREADS, 1)
     br_kernel(const uint64_t *__restrict__ lwe_in, int n, const uint64_t *__restrict__ lut, int n_out,
               const cplx *__restrict__ ggsw_base, int n_in, uint64_t *__restrict__ out, long B,
               uint64_t body_add, uint64_t out_add, const cplx *__restrict__ twist, const cplx *__restrict__ wtab,
-              const double *__restrict__ lf, uint64_t *__restrict__ clk) {
+              const double *__restrict__ lf, uint64_t *__restrict__ clk, long lut_mod = 1) {
     constexpr int LOGN = 9;
     ClockStamp stamp;
     stamp.start(clk);
@@ -234,7 +234,8 @@ __global__ void __launch_bounds__(THREADS, 1)
                 const uint64_t *in = lwe_in + (size_t)(ct0 + ct) * (n + 1);
                 const int bt = mod_switch(in[n] + body_add, LOGN);
                 const int e0 = (2 * N - (bt % (2 * N))) % (2 * N);
-                v = rotated_coeff(lut + c * N, j, e0, N);
+                // PBS: the test vector of ciphertext ct0 + ct (lut_mod > 1: one per ciphertext, shortint_1bit)
+                v = rotated_coeff(lut + ((ct0 + ct) % lut_mod) * (K1 * N) + c * N, j, e0, N);
             } else {
                 v = c < K1 - 1 ? 0 : lut[(size_t)(ct0 + ct) * N + j];
             }

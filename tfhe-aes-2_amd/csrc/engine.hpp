@@ -229,6 +229,8 @@ class Engine {
     size_t br1024lat_lds_ = 0;
     bool x4_512_ = false;     // PBS N = 512, k = 4, 3 x 2^12 (lvl_64): br512x4 / br512lat on the fused transform
     bool x4_vp_ = false;      // ... and cbs 1 x 2^13: vertical packing on br512x4<1, false, 13>
+    bool lf512_ = false;      // N = 512, k = 4: the fused transform, conj(E2)-rescaled BSK (oracle lf_set)
+    bool x4_s1_ = false;      // shortint_1bit PBS 7 x 2^6: br512x4<7, true, 6> with per-ciphertext test vectors
     long lat_max_ = 256;      // batch size up to which br512lat runs (TAE_BR_LAT_MAX)
     int num_cu_ = 256;
     double *d_lf_ = nullptr;  // the fused-twiddle transform's table (lf512.hpp: params_sqrd_lvl_64, lf1k.hpp: 8-bit)

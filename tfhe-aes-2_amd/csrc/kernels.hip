@@ -753,12 +753,19 @@ void Engine::init_common() {
     // to which br512lat runs (0: never).
     // The PBS shape alone decides the fused transform and its conj(E2)-rescaled BSK, exactly as the oracle's
     // lf_set (tfhe_oracle.c); the vertical-packing instantiation br512x4<1, false, 13> also needs cbs 1 x 2^13.
-    x4_512_ = p_.N == 512 && p_.k == 4 && p_.pbs_l == 3 && p_.pbs_b == 12;
+    // The fused transform and its conj(E2)-rescaled BSK go with the blind rotation's N = 512, k = 4 shape,
+    // exactly as the oracle's lf_set (tfhe_oracle.c): params_sqrd_lvl_64 (3 x 2^12: br512x4 / br512lat) and
+    // the shortint_1bit set (7 x 2^6, per-ciphertext test vectors: br512x4 only); the vertical-packing
+    // instantiation br512x4<1, false, 13> also needs cbs 1 x 2^13.
+    lf512_ = p_.N == 512 && p_.k == 4;
+    x4_512_ = lf512_ && p_.pbs_l == 3 && p_.pbs_b == 12;
+    x4_s1_ = lf512_ && p_.pbs_l == 7 && p_.pbs_b == 6;
+    if (lf512_ && !x4_512_ && !x4_s1_) throw std::runtime_error("N = 512, k = 4 set without a blind rotation kernel");
     x4_vp_ = x4_512_ && p_.cbs_l == 1 && p_.cbs_b == 13;
     // the 8-bit model's set: its PBS blind rotations run the N = 1024 fused-twiddle transform (lf1k.hpp)
     lf1k_ = p_.N == 1024 && p_.k == 2 && p_.pbs_l == 6 && p_.pbs_b == 7;
-    if (x4_512_ || lf1k_) {  // the blind rotations' fused-twiddle transform (lf512.hpp / lf1k.hpp)
-        const std::vector<double> lf = x4_512_ ? make_lf512_table() : make_lf1k_table();
+    if (lf512_ || lf1k_) {  // the blind rotations' fused-twiddle transform (lf512.hpp / lf1k.hpp)
+        const std::vector<double> lf = lf512_ ? make_lf512_table() : make_lf1k_table();
         d_lf_ = static_cast<double *>(alloc(lf.size() * 8));
         HIPC(hipMemcpy(d_lf_, lf.data(), lf.size() * 8, hipMemcpyHostToDevice));
     }
@@ -773,6 +780,9 @@ void Engine::init_common() {
     }
     if (x4_vp_)
         HIPC(hipFuncSetAttribute((const void *)br512x4::br_kernel<1, false, 13>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    if (x4_s1_)
+        HIPC(hipFuncSetAttribute((const void *)br512x4::br_kernel<7, true, 6>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     // batched N=1024, k=2 blind rotation (br1024.hpp); other shapes run the generic kernels
     if (p_.N == 1024 && p_.k == 2) {
@@ -837,8 +847,8 @@ void Engine::bsk_to_fourier(const uint64_t *d_bsk_std) {
             d_bsk_std, d_bsk_f_, polys, d_twist_, d_w_);
     }
     HIPC(hipGetLastError());
-    if (x4_512_ || lf1k_) {  // the blind rotations run the fused-twiddle transform: its BSK carries conj(E2)
-        const cplx *e2 = reinterpret_cast<const cplx *>(d_lf_ + (x4_512_ ? lf512::E2 : lf1k::E2));
+    if (lf512_ || lf1k_) {  // the blind rotations run the fused-twiddle transform: its BSK carries conj(E2)
+        const cplx *e2 = reinterpret_cast<const cplx *>(d_lf_ + (lf512_ ? lf512::E2 : lf1k::E2));
         lf_rescale_kernel<<<grid_for(polys * M), kThreads, 0, stream_>>>(d_bsk_f_, polys, M, e2);
         HIPC(hipGetLastError());
     }
@@ -1012,7 +1022,17 @@ void Engine::bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint
     if (!B) return;
     if (lut_mod == 0) throw std::runtime_error("bootstrap: lut_mod must be >= 1");
     if (lut_mod > 1 && (x4_512_ || br1024_pbs_ || br1024lat_))
-        throw std::runtime_error("per-ciphertext test vectors run on the generic blind rotation only");
+        throw std::runtime_error("per-ciphertext test vectors run on br512x4<7, true, 6> or the generic blind rotation");
+    if (x4_s1_) {
+        // shortint_1bit (7 levels of 2^6, per-ciphertext test vectors): three ciphertexts per workgroup at any
+        // batch size (br512lat runs the three levels of params_sqrd_lvl_64 in parallel and has no 7-level form)
+        const unsigned wgs = (unsigned)((B + 2) / 3);
+        br512x4::br_kernel<7, true, 6><<<wgs, br512x4::THREADS, br512x4::lds_bytes(), stream_>>>(
+            d_small, p_.n, d_lut_glwe, 0, d_bsk_f_, 0, d_big, (long)B, body_add, out_add, d_twist_, d_w_, d_lf_, nullptr,
+            (long)lut_mod);
+        HIPC(hipGetLastError());
+        return;
+    }
     if (x4_512_) {
         if ((long)B <= lat_max_) {
             br512lat::br_kernel<3, 12><<<(unsigned)B, br512lat::THREADS, br512lat::lds_bytes(3), stream_>>>(
