@@ -64,12 +64,15 @@ __global__ void __launch_bounds__(1024, 1) k(double *out, int iters, const cplx 
     __syncthreads();
     constexpr int LPJ = 64 / (P / 4) / 1;  // lanes per job: 64, 32, 16
     constexpr int JPW = 64 / LPJ;          // jobs per wave
+    // P = 4 with NJ = 30: every job wave runs two jobs back to back between the barriers (SEQ = 2)
+    constexpr int SEQ = (P == 4 && NJ > JOBS) ? NJ / JOBS : 1;
     const int job = wave * JPW + lane / LPJ;
-    const bool busy = wave * JPW < NJ;  // wave-uniform (a partial last wave computes a dummy job)
+    const bool busy = wave * JPW < (SEQ > 1 ? JOBS : NJ);  // wave-uniform (a partial last wave: a dummy job)
     // NJ > 15 (what-if, timing only): jobs share the 15 LDS regions
     cplx *X = buf + (job % JOBS) * STRIDE;
     const int u = lane & 15;
     for (int it = 0; it < iters; it++) {
+      for (int sq = 0; sq < SEQ; sq++)
         if (busy) {
             if constexpr (P == 4) {
                 const int r = (lane >> 4) & 3;
@@ -212,7 +215,10 @@ int main() {
     run<16>(d, tw, cus, iters, ghz);
     run<4>(d, tw, cus, iters, ghz);
     // what-if: as many jobs as the 16 waves hold (LDS regions shared, timing only)
+    run<4, 30>(d, tw, cus, iters, ghz);
     run<8, 30>(d, tw, cus, iters, ghz);
+    run<16, 30>(d, tw, cus, iters, ghz);
+    run<16, 45>(d, tw, cus, iters, ghz);
     run<16, 60>(d, tw, cus, iters, ghz);
     return 0;
 }
