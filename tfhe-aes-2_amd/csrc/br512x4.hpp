@@ -280,7 +280,10 @@ __global__ void __launch_bounds__(THREADS, 1)
         // ---- rotated difference + decomposition of coefficients j = u + 16 r + 64 i (+ M) ----
         int ll = lane;
         asm volatile("" : "+v"(ll));
-        uint32_t dig[LEV][4];
+        // digits of all levels: 16-bit pairs (decompose16p), or for deep decompositions of at most 7-bit
+        // digits (shortint_1bit: 7 levels of 2^6) byte pairs, two levels per dword (16 instead of 28 VGPRs)
+        constexpr bool DBYTES = PBS && LEV > 3 && BLOG <= 7;
+        uint32_t dig[DBYTES ? (LEV + 1) / 2 : LEV][4];
         if (fjob) {
             const uint64_t *poly = acc + jb * ACC_STRIDE;
             // coefficient j of ACC * X^e is entry t = (j - e) mod 2N of [ACC, -ACC]
@@ -298,8 +301,16 @@ __global__ void __launch_bounds__(THREADS, 1)
                 // both halves at once with 16-bit SIMD ops (fft_device.hpp decompose16p)
                 uint32_t dp[LEV];
                 decompose16p<LEV, BLOG>(x0, x1, dp);
+                if constexpr (DBYTES) {
 #pragma unroll
-                for (int l = 0; l < LEV; l++) dig[l][i] = dp[l];
+                    for (int l = 0; l < LEV; l += 2) {  // bytes 0, 1: level l (j, j + M); bytes 2, 3: level l + 1
+                        const uint32_t up = l + 1 < LEV ? dp[(l + 1) % LEV] : 0u;
+                        dig[l >> 1][i] = __builtin_amdgcn_perm(up, dp[l], 0x06040200u);
+                    }
+                } else {
+#pragma unroll
+                    for (int l = 0; l < LEV; l++) dig[l][i] = dp[l];
+                }
             }
         }
 #pragma unroll
@@ -314,16 +325,31 @@ __global__ void __launch_bounds__(THREADS, 1)
                 // fused-twiddle transform (lf512.hpp): pass A = DFT4 of the twisted digits, transpose, fused
                 // DFT4 -> LDS position u + 16 k (its W_M^{u k} and psi^u factors ride into pass B)
                 if (fjob) {
-                    uint32_t dw[4];
-#pragma unroll
-                    for (int i = 0; i < 4; i++) {
-                        dw[i] = dig[0][i];
-#pragma unroll
-                        for (int l = 1; l < LEV; l++)
-                            if (lev - 1 == l) dw[i] = dig[l][i];
-                    }
                     cplx v[4];
-                    lf512::a1(dw, v, lf_s2, lf_c8, lf_t8);
+                    if constexpr (DBYTES) {
+                        const int sh = ((lev - 1) & 1) * 16;  // lev is a compile-time constant (unrolled)
+                        int dr[4], di[4];
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            uint32_t dw = dig[0][i];
+#pragma unroll
+                            for (int w = 1; w < (LEV + 1) / 2; w++)
+                                if ((lev - 1) >> 1 == w) dw = dig[w][i];
+                            dr[i] = __builtin_amdgcn_sbfe((int)dw, sh, 8);
+                            di[i] = __builtin_amdgcn_sbfe((int)dw, sh + 8, 8);
+                        }
+                        lf512::a1i(dr, di, v, lf_s2, lf_c8, lf_t8);
+                    } else {
+                        uint32_t dw[4];
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            dw[i] = dig[0][i];
+#pragma unroll
+                            for (int l = 1; l < LEV; l++)
+                                if (lev - 1 == l) dw[i] = dig[l][i];
+                        }
+                        lf512::a1(dw, v, lf_s2, lf_c8, lf_t8);
+                    }
                     br512::transpose4(v);
                     lf512::dft4<false>(v, lf512::k4(s_lf, lf512::FA2, 4, r));
                     if (lev == LEV) PRIO(2);

@@ -67,11 +67,10 @@ __device__ __forceinline__ void dft4(cplx *x, const K4 &K) {
 
 // forward pass A stage 1: DFT4 over i of d_i psi^(64 i) for the packed digit pairs dw[i] (low half: the
 // coefficient j, high half: j + 256), outputs k1 = 0..3 in natural order
-__device__ __forceinline__ void a1(const uint32_t *dw, cplx *q, double s2, double c8, double t8) {
-    const int d0r = (int32_t)(dw[0] << 16) >> 16, d0i = (int32_t)dw[0] >> 16;
-    const int d1r = (int32_t)(dw[1] << 16) >> 16, d1i = (int32_t)dw[1] >> 16;
-    const int d2r = (int32_t)(dw[2] << 16) >> 16, d2i = (int32_t)dw[2] >> 16;
-    const int d3r = (int32_t)(dw[3] << 16) >> 16, d3i = (int32_t)dw[3] >> 16;
+// (digits as ints: dr[i] of the coefficient j, di[i] of j + 256)
+__device__ __forceinline__ void a1i(const int *dr, const int *di, cplx *q, double s2, double c8, double t8) {
+    const int d0r = dr[0], d0i = di[0], d1r = dr[1], d1i = di[1];
+    const int d2r = dr[2], d2i = di[2], d3r = dr[3], d3i = di[3];
     const double D0r = d0r, D0i = d0i, D1r = d1r, D1i = d1i;
     const double P2r = d2r - d2i, P2i = d2r + d2i, P3r = d3r - d3i, P3i = d3r + d3i;  // e^{i pi/4} sqrt 2 d
     const cplx ep = {fma(s2, P2r, D0r), fma(s2, P2i, D0i)}, em = {fma(-s2, P2r, D0r), fma(-s2, P2i, D0i)};
@@ -81,6 +80,15 @@ __device__ __forceinline__ void a1(const uint32_t *dw, cplx *q, double s2, doubl
     q[2] = addc(ep, -c8, a);
     q[1] = {fma(c8, b.im, em.re), fma(-c8, b.re, em.im)};
     q[3] = {fma(-c8, b.im, em.re), fma(c8, b.re, em.im)};
+}
+__device__ __forceinline__ void a1(const uint32_t *dw, cplx *q, double s2, double c8, double t8) {
+    int dr[4], di[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        dr[i] = (int32_t)(dw[i] << 16) >> 16;
+        di[i] = (int32_t)dw[i] >> 16;
+    }
+    a1i(dr, di, q, s2, c8, t8);
 }
 
 }  // namespace lf512
