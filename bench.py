@@ -33,7 +33,7 @@ HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (= FP64 matrix) dense peak, spec
 SPEC_CLOCK_GHZ = 2.4      # the clock the spec peaks assume
 FP64_SUSTAINED_TFLOPS = 58.0  # measured sustained v_fma_f64 rate, all CUs (scripts/probes/fp64_peak.hip)
-PBS_KERNELS = {"1bit": "tae::br512x4::br_kernel<3, true, 12>", "8bit": "tae::br1024::br_kernel<6, true, 7, 2, 1>"}
+PBS_KERNELS = {"1bit": "tae::br512x4::br_kernel<3, true, 12>", "8bit": "tae::br1024::br_kernel<6, true, 7, 2, 1, 1>"}
 
 
 def pbs_algorithmic(p, bits):
@@ -279,12 +279,22 @@ def main():
     # -> scripts/prof_summary.py: 2 x FETCH_SIZE + WRITE_SIZE), valid only for the same batch shape.
     traffic, traffic_src = None, None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_latest.json")
-    if os.path.exists(pmc_path):
+    if args.model == "1bit" and os.path.exists(pmc_path):
         with open(pmc_path) as fh:
             pm = json.load(fh)
         ent = pm.get("kernels", {}).get(PBS_KERNEL, {})
         if pm.get("blocks_per_gpu") == nb and "hbm_bytes_per_launch" in ent:
             traffic, traffic_src = ent["hbm_bytes_per_launch"], pm.get("source")
+    pmc8_path = os.path.join(ROOT, "profiles", "pmc8_latest.json")
+    if args.model == "8bit" and os.path.exists(pmc8_path):
+        # scripts/prof8.sh -> scripts/prof_split_summary.py, split per launch shape: the CBS launch is the
+        # kernel's largest grid
+        with open(pmc8_path) as fh:
+            pm = json.load(fh)
+        ents = [e for e in pm.get("launches", {}).values() if e.get("kernel") == PBS_KERNEL]
+        ent = max(ents, key=lambda e: e["grid_threads"]) if ents else {}
+        if pm.get("blocks_per_gpu") == nb and "traffic_bytes_per_launch" in ent:
+            traffic, traffic_src = ent["traffic_bytes_per_launch"], pm.get("source")
     # The batched blind rotation is bound by the FP64 vector ALU (>= 10 flop/B at any
     # batch; no MFMA on this path): peak = the dense FP64 vector rate, HBM figures ride along.
     roofline = {"bound": "fp64_valu", "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -297,7 +307,8 @@ def main():
                 "algorithmic_flop_per_launch": k_flop,
                 "stage": {"avg_ms": pbs_ms, "ciphertexts": nb * 16 * 8, "achieved": stage_tflops,
                           "frac": (stage_tflops / FP64_PEAK_TFLOPS) if stage_tflops else None,
-                          "note": "whole PBS stage per launch: the kernel above + the br512lat remainder"},
+                          "note": ("whole PBS stage per launch: the kernel above + the br512lat remainder" if main_ms > 0
+                                   else "whole PBS stage per launch: the kernel above alone")},
                 "hbm": {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": (gbs / HBM_PEAK_GBS) if gbs else None,
                         "algorithmic_bytes_per_launch": k_bytes},
@@ -451,7 +462,7 @@ def model8_leg(torch, dev, nb, threads, steps=3):
     _, flop_launch = pbs_algorithmic(tfhe_aes.get_params(pid), nb * 16 * 8)
     pbs_ms, launches = stages.get("pbs", 0.0), stages.get("pbs_launches", 0)
     tf = launches * flop_launch / (pbs_ms * 1e-3) / 1e12 if pbs_ms and launches else None
-    cbs_roofline = {"bound": "fp64_valu", "kernel": "tae::br1024::br_kernel<6, true, 7, 2, 1> (CBS PBS)",
+    cbs_roofline = {"bound": "fp64_valu", "kernel": PBS_KERNELS["8bit"] + " (CBS PBS)",
                     "achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": (tf / FP64_PEAK_TFLOPS) if tf else None, "launches_per_step": launches,
                     "algorithmic_flop_per_launch": flop_launch,
