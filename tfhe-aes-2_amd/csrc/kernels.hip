@@ -751,8 +751,6 @@ void Engine::init_common() {
     // batched N=512, k=4 blind rotation (params_sqrd_lvl_64): br512x4 for large batches, br512lat for
     // small ones.  TAE_BR_LAT_MAX (a tuning knob, both sides pinned by tests) is the batch size up
     // to which br512lat runs (0: never).
-    // The PBS shape alone decides the fused transform and its conj(E2)-rescaled BSK, exactly as the oracle's
-    // lf_set (tfhe_oracle.c); the vertical-packing instantiation br512x4<1, false, 13> also needs cbs 1 x 2^13.
     // The fused transform and its conj(E2)-rescaled BSK go with the blind rotation's N = 512, k = 4 shape,
     // exactly as the oracle's lf_set (tfhe_oracle.c): params_sqrd_lvl_64 (3 x 2^12: br512x4 / br512lat) and
     // the shortint_1bit set (7 x 2^6, per-ciphertext test vectors: br512x4 only); the vertical-packing
