@@ -1,6 +1,7 @@
-// Batched blind rotation for N = 512, k = 4 (params_sqrd_lvl_64) with FOUR waves per SIMD:
-// 1024-thread workgroups, C = 3 ciphertexts each, ACC and one level of spectra in LDS, every GGSW
-// value loaded from L2 feeding three accumulators.
+// Batched blind rotation for N = 512, k = 4 with FOUR waves per SIMD: 1024-thread workgroups, C = 3
+// ciphertexts each, ACC and one level of spectra in LDS, every GGSW value loaded from L2 feeding three
+// accumulators.  Instantiations: <3, true, 12> the PBS of params_sqrd_lvl_64, <7, true, 6> the
+// shortint_1bit bootstrap (a test vector per ciphertext, lut_mod), <1, false, 13> vertical packing.
 //
 // Every FFT job (ciphertext, polynomial) is one whole wave: lane (u, r) = (lane & 15, lane >> 4)
 // holds the four points x[r + 4 i] of column (or row) u of the 16 x 16 FFT.  A DFT16 runs as
