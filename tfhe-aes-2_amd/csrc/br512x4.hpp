@@ -558,5 +558,18 @@ inline size_t lds_bytes() {
     return (size_t)JOBS * ACC_STRIDE * 8 + (size_t)JOBS * BUF_STRIDE * 16 + 3 * (size_t)M * 16 + 12 * 16;
 }
 
+// The instantiations are compiled in their own translation unit (br512x4_inst.hip) with the post-RA machine
+// scheduler off (-mllvm --enable-post-misched=false: -0.7 to -1.1% per launch, same box; the other kernels
+// lose 2-4% with it); every other file sees them through these extern declarations.
+#define TAE_X4_PARAMS                                                                                         \
+    const uint64_t *__restrict__, int, const uint64_t *__restrict__, int, const cplx *__restrict__, int,    \
+        uint64_t *__restrict__, long, uint64_t, uint64_t, const cplx *__restrict__, const cplx *__restrict__, \
+        const double *__restrict__, uint64_t *__restrict__, long
+#ifndef TAE_X4_INSTANTIATE
+extern template __global__ void br_kernel<3, true, 12>(TAE_X4_PARAMS);
+extern template __global__ void br_kernel<7, true, 6>(TAE_X4_PARAMS);
+extern template __global__ void br_kernel<1, false, 13>(TAE_X4_PARAMS);
+#endif
+
 }  // namespace br512x4
 }  // namespace tae
