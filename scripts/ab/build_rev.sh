@@ -13,12 +13,15 @@ mkdir -p dbg
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off -w --offload-arch=gfx950 -munsafe-fp-atomics "$@" \
   -c "$tmp/tfhe-aes-2_amd/csrc/kernels.hip" -o dbg/$name.o
 objs=dbg/$name.o
-if [ -f "$tmp/tfhe-aes-2_amd/csrc/br512x4_inst.hip" ]; then  # revisions with br512x4 in its own unit
-  x4=$(git -C "$ROOT" show "$rev:tfhe-aes-2_amd/Makefile" | sed -n 's/^X4FLAGS = //p')
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off -w --offload-arch=gfx950 -munsafe-fp-atomics $x4 "$@" \
-    -c "$tmp/tfhe-aes-2_amd/csrc/br512x4_inst.hip" -o dbg/$name.x4.o
-  objs="$objs dbg/$name.x4.o"
-fi
+# revisions with kernels in units of their own: each built with its Makefile flag variable
+for unit in br512x4_inst:X4FLAGS br512lat_inst:LATFLAGS; do
+  src=${unit%%:*}; var=${unit#*:}
+  [ -f "$tmp/tfhe-aes-2_amd/csrc/$src.hip" ] || continue
+  fl=$(git -C "$ROOT" show "$rev:tfhe-aes-2_amd/Makefile" | sed -n "s/^$var = //p")
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off -w --offload-arch=gfx950 -munsafe-fp-atomics $fl "$@" \
+    -c "$tmp/tfhe-aes-2_amd/csrc/$src.hip" -o dbg/$name.$src.o
+  objs="$objs dbg/$name.$src.o"
+done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o dbg/$name.so $objs build/client.o build/model.o build/capi.o build/keyio.o -lpthread
-rm -rf dbg/$name.o dbg/$name.x4.o "$tmp"
+rm -rf $objs "$tmp"
 echo "dbg/$name.so from $rev"

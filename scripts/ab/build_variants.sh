@@ -6,16 +6,21 @@ set -e
 cd "$(dirname "$0")/../../tfhe-aes-2_amd"
 make -s
 mkdir -p dbg
-X4FLAGS=$(make -s --no-print-directory -f Makefile -f - <<<'print-x4: ; @echo $(X4FLAGS)' print-x4)
+# the kernel units and their Makefile flag variables (kernels.hip: none)
+mkvar() { make -s --no-print-directory -f Makefile -f - <<<"print-var: ; @echo \$($1)" print-var; }
+X4FLAGS=$(mkvar X4FLAGS); LATFLAGS=$(mkvar LATFLAGS)
+HC="/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off -w --offload-arch=gfx950 -munsafe-fp-atomics"
 for spec in "$@"; do
   name=${spec%%=*}; flags=${spec#*=}
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off -w --offload-arch=gfx950 -munsafe-fp-atomics $flags -c csrc/kernels.hip -o dbg/$name.o &
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off -w --offload-arch=gfx950 -munsafe-fp-atomics $X4FLAGS $flags -c csrc/br512x4_inst.hip -o dbg/$name.x4.o &
+  $HC $flags -c csrc/kernels.hip -o dbg/$name.o &
+  $HC $X4FLAGS $flags -c csrc/br512x4_inst.hip -o dbg/$name.x4.o &
+  $HC $LATFLAGS $flags -c csrc/br512lat_inst.hip -o dbg/$name.lat.o &
 done
 wait
 for spec in "$@"; do
   name=${spec%%=*}
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o dbg/$name.so dbg/$name.o dbg/$name.x4.o build/client.o build/model.o build/capi.o build/keyio.o -lpthread
-  rm dbg/$name.o dbg/$name.x4.o
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o dbg/$name.so dbg/$name.o dbg/$name.x4.o dbg/$name.lat.o \
+    build/client.o build/model.o build/capi.o build/keyio.o -lpthread
+  rm dbg/$name.o dbg/$name.x4.o dbg/$name.lat.o
 done
 ls dbg

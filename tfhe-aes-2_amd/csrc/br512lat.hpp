@@ -295,6 +295,15 @@ __global__ void __launch_bounds__(THREADS, 1)
     if (tid == 0) o[(K1 - 1) * N] = acc[(K1 - 1) * N] + out_add;
 }
 
+// The instantiation is compiled in its own translation unit (br512lat_inst.hip) with top-down pre-RA machine
+// scheduling (Makefile LATFLAGS: -6% per launch, same box; br1024 and the PFKS GEMM lose with it).
+#define TAE_LAT_PARAMS                                                                                      \
+    const uint64_t *__restrict__, int, const uint64_t *__restrict__, const cplx *__restrict__,            \
+        uint64_t *__restrict__, long, uint64_t, uint64_t, const double *__restrict__
+#ifndef TAE_LAT_INSTANTIATE
+extern template __global__ void br_kernel<3, 12>(TAE_LAT_PARAMS);
+#endif
+
 inline size_t lds_bytes(int lev) {
     return (size_t)K1 * N * 8 + (size_t)(lev * K1 + K1) * BUF_STRIDE * 16 + (size_t)lf512::KERNEL_DOUBLES * 8 +
            (size_t)lev * K1 * M * 4;
