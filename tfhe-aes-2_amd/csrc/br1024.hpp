@@ -552,15 +552,22 @@ inline size_t lds_bytes(int C, int LP = 1, bool lft = false) {
 // (levels, base_log) combinations of the N=1024 parameter sets: returns the kernel or nullptr
 typedef void (*kernel_t)(const uint64_t *, int, const uint64_t *, int, const cplx *, int, uint64_t *, long, uint64_t,
                          uint64_t, const cplx *, const cplx *, const cplx *, const double *, uint64_t *);
+// The kernels are instantiated in their own translation unit (br1024_inst.hip, Makefile B1KFLAGS: -O2 there is
+// -0.7% per 8192-bootstrap launch, same box); other files reach them through these selectors.
 // the 8-bit model's PBS as one ciphertext per workgroup at two workgroups per CU (OCC = 2)
-inline kernel_t pick_occ2(int levels, int base_log) {
+kernel_t pick_occ2(int levels, int base_log);
+// LP levels per pass; LP = 2 only for the PBS with at least two passes (nullptr otherwise)
+template <int C, int LP = 1>
+kernel_t pick(bool pbs, int levels, int base_log);
+
+#ifdef TAE_B1K_INSTANTIATE
+kernel_t pick_occ2(int levels, int base_log) {
     if (levels == 6 && base_log == 7) return (kernel_t)br_kernel<6, true, 7, 1, 1, 2>;
     return nullptr;
 }
 
-// LP levels per pass; LP = 2 only for the PBS with at least two passes (nullptr otherwise)
-template <int C, int LP = 1>
-inline kernel_t pick(bool pbs, int levels, int base_log) {
+template <int C, int LP>
+kernel_t pick(bool pbs, int levels, int base_log) {
 #define TAE_BR1024(L, BL)                                                                                  \
     if constexpr (LP == 1)                                                                                 \
         if (levels == L && base_log == BL)                                                                 \
@@ -577,6 +584,11 @@ inline kernel_t pick(bool pbs, int levels, int base_log) {
 #undef TAE_BR1024
     return nullptr;
 }
+
+template kernel_t pick<2, 1>(bool, int, int);
+template kernel_t pick<1, 1>(bool, int, int);
+template kernel_t pick<1, 2>(bool, int, int);
+#endif
 
 }  // namespace br1024
 }  // namespace tae
