@@ -209,6 +209,9 @@ def main():
     got = aes_128.bits_to_blocks(ck.decrypt_bits_raw(out))
     ek_plain = aes_128.key_schedule_plain(README_KEY)
     ok = int(all(g == aes_128.encrypt_block_plain(ek_plain, b, args.rounds) for g, b in zip(got, blocks)))
+    if not clock_step_identical:  # the stamped step must reproduce the timed steps' ciphertexts bit for bit
+        print(f"rank {rank}: the clock-stamped step's ciphertexts differ from the timed steps'", file=sys.stderr)
+        ok = 0
     if dist:
         ok = D.min_over_ranks(dist, ok, f"cuda:{dev}")
     if not ok:
@@ -456,6 +459,9 @@ def model8_leg(torch, dev, nb, threads, steps=3):
     got = aes_128.bits_to_blocks(ck.decrypt_bits_raw(out))
     ek_plain = aes_128.key_schedule_plain(README_KEY)
     correct = all(g == aes_128.encrypt_block_plain(ek_plain, b, 10) for g, b in zip(got, blocks))
+    if not clock_step_identical:
+        print("model8: the clock-stamped step's ciphertexts differ from the timed steps'", file=sys.stderr)
+        correct = False
     del ctx, clk_out
     # the circuit bootstrap's PBS launches (one per CBS level and round, nb x 16 x 8 bits each): the
     # dominant kernel of this model, against the same FP64 spec as the headline line

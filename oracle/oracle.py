@@ -342,8 +342,8 @@ class S1Keys(Keys):
     """shortint_1bit model (param id 5, src/tfhe/shortint_1bit.rs): bits are shortint ciphertexts under the
     SMALL key [n+1], test vectors are GLWEs [(k+1)N]."""
 
-    def __init__(self, seed: bytes, threads: int = 8, raw=None):
-        super().__init__(PARAMS_SHORTINT_1BIT, seed, threads, raw)
+    def __init__(self, seed: bytes, threads: int = 8, raw=None, transform: str = "product"):
+        super().__init__(PARAMS_SHORTINT_1BIT, seed, threads, raw, transform)
         self.L = self.p["n"] + 1
         self.G = (self.p["k"] + 1) * self.p["N"]
 
@@ -382,6 +382,14 @@ class S1Keys(Keys):
         out = np.zeros(self.G, dtype=np.uint64)
         lib().or_s1_tv_from_cts(self.sk, _p64(np.ascontiguousarray(ct0, dtype=np.uint64)),
                                 _p64(np.ascontiguousarray(ct1, dtype=np.uint64)), _p64(out))
+        return out
+
+    def bootstrap_big(self, ct: np.ndarray, tv: np.ndarray) -> np.ndarray:
+        """apply_programmable_bootstrap alone (blind rotation + sample extraction, before the keyswitch):
+        the big-key LWE [k N + 1]"""
+        out = np.zeros(self.K + 1, dtype=np.uint64)
+        lib().or_bootstrap(self.sk, _p64(np.ascontiguousarray(ct, dtype=np.uint64)),
+                           _p64(np.ascontiguousarray(tv, dtype=np.uint64)), _p64(out))
         return out
 
     def bootstrap(self, ct: np.ndarray, tv: np.ndarray) -> np.ndarray:

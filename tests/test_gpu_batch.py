@@ -53,6 +53,23 @@ def test_full_batch_128_blocks_two_rounds(gpu_context, oracle_keys, client, read
         assert np.array_equal(out[b], ref), b
 
 
+def test_full_batch_128_blocks_ten_rounds(gpu_context, oracle_keys, client, readme_setup):
+    """The headline shape word for word through all 10 rounds (test_full_gal_mul,
+    fhe_impls/shortint_woppbs_1bit.rs:195-210, at bench.py's 128 blocks): one batched call, every CBS
+    launch 21 rounds of br512x4 + the br512lat remainder; all blocks decrypt to AES-128, and blocks 0,
+    126 (the first past the br512x4 / remainder split) and 127 equal the oracle's 10-round output."""
+    key, iv, rk = readme_setup
+    nb = 128
+    blocks = aes_128.counter_blocks(iv, nb)
+    cts = client.encrypt_bits_raw(aes_128.blocks_to_bits(blocks), start_index=800_000).reshape(nb, 128, BIG)
+    out = E.encrypt_blocks_raw(gpu_context, rk, cts, rounds=10)
+    got = aes_128.bits_to_blocks(client.decrypt_bits_raw(out))
+    assert got == aes_128.expand_key_and_encrypt_blocks(key, blocks, 10)
+    for b in (0, 126, nb - 1):
+        ref = oracle_keys.aes_encrypt_block(rk, cts[b], 10, threads=16)
+        assert np.array_equal(out[b], ref), b
+
+
 def test_1024_blocks_one_call_one_round(gpu_context, oracle_keys, client, readme_setup):
     """BASELINE's largest N (1024 counter-mode blocks) in ONE call on one GPU: each CBS launch is
     1024 x 16 x 8 = 131072 PBS (43691 br512x4 workgroups, the last one holding two ciphertexts: the

@@ -5,6 +5,7 @@ per workgroup, so output counts that are not multiples of 3 and single-group bat
 partial workgroups; every output is compared with the oracle or decrypted.
 """
 import ctypes as C
+import os
 
 import numpy as np
 import pytest
@@ -165,12 +166,25 @@ def test_context_shared_across_host_threads(gpu_context, client):
         assert np.array_equal(par[t], seq[t]), t
 
 
+def _pbs_main_cts(B):
+    """The ciphertexts Engine::bootstrap gives the throughput kernel for a batch of B (kernels.hip): whole
+    rounds of 3 x CUs, a remainder of at most min(TAE_BR_LAT_MAX, CUs) going to br512lat."""
+    import torch
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    lat_max = int(os.environ.get("TAE_BR_LAT_MAX", "256"))
+    if B <= lat_max:
+        return 0
+    per_round = 3 * cus
+    rest = B % per_round
+    return B - rest if (B > per_round and 0 < rest <= min(lat_max, cus)) else B
+
+
 def test_timing_modes_bit_identical(gpu_context, client):
     """tae_set_timing: mode 1 (HIP events per stage) and mode 2 (plus the in-kernel clock stamps of the
     throughput blind rotation, bench.py's effective_clock_ghz) leave the ciphertexts of a batched call
     bit-identical to mode 0; mode 2 fills the clock fields with a plausible shader clock; mode 3 is
     TAE_E_ARG (before mode 2 existed any nonzero value meant "on").  8 blocks x 1 round: one SubBytes
-    circuit bootstrap of 1024 bits = one br512x4 launch of 768 + a br512lat remainder of 256."""
+    circuit bootstrap of 1024 bits (on 256 CUs: one br512x4 launch of 768 + a br512lat remainder of 256)."""
     E = aes_128.ShortintWoppbs1BitSboxGalMulPbsAesEncrypt
     rk = client.encrypt_bits_raw([(i * 5 + 1) >> 1 & 1 for i in range(1408)], start_index=7_000_000)
     nb = 8
@@ -185,7 +199,7 @@ def test_timing_modes_bit_identical(gpu_context, client):
         N.check(N.lib().tae_set_timing(gpu_context._h, 0))
     assert np.array_equal(outs[1][0], outs[0][0]) and np.array_equal(outs[2][0], outs[0][0])
     t1, t2 = outs[1][1], outs[2][1]
-    assert t1["pbs"] > 0 and t1["pbs_main"] > 0 and t1["pbs_main_cts"] == 768 and "pbs_clock_ghz" not in t1, t1
+    assert t1["pbs"] > 0 and t1["pbs_main"] > 0 and t1["pbs_main_cts"] == _pbs_main_cts(128 * nb) and "pbs_clock_ghz" not in t1, t1
     assert t2["pbs_clock_launches"] >= 1 and 1.0 < t2["pbs_clock_ghz"] < 3.0, t2
     assert N.lib().tae_set_timing(gpu_context._h, 3) == N.TAE_E_ARG
     assert N.lib().tae_set_timing(gpu_context._h, -1) == N.TAE_E_ARG

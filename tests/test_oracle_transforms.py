@@ -69,6 +69,36 @@ def test_pbs_fused_vs_radix(oracle_mod, oracle_keys, oracle_keys8, which):
     assert ef.var() <= 1.0 * er.var(), (ef.var() / er.var())
 
 
+def test_pbs_fused_vs_radix_shortint1(oracle_mod):
+    """The shortint_1bit set (N 512, k 4, 7 levels of 2^6) runs the same fused transform as lvl_64 on the
+    product (br512x4<7, true, 6>) and in the oracle (lf_set).  Tie that deep decomposition back to the radix
+    schedule: apply_programmable_bootstrap (shortint_1bit.rs:264-294, before its keyswitch) with a test
+    vector per ciphertext (test_vector_from_cleartext_fn, :365-390), 128 random bits and functions.
+    Outputs are 2-bit shortints (message + carry, delta 2^62), so errors are taken mod 2^63; margin 2^61.
+    Measured: max errors 2^33.3 / 2^34.0 (fused / radix), phase difference < 2^34.3, variance ratio 0.88."""
+    keys = oracle_mod.S1Keys(bytes(range(32)), threads=THREADS)
+    radix = oracle_mod.S1Keys(None, raw=keys.raw_server(), transform="radix")
+    rng = np.random.default_rng(19)
+    n = 128
+    bits, f0, f1 = (rng.integers(0, 2, n) for _ in range(3))
+    cts = keys.s1_encrypt(bits, b"\x77" * 32, 2000)
+    tvs = [keys.tv_from_fn(int(a), int(b)) for a, b in zip(f0, f1)]
+    with ThreadPoolExecutor(THREADS) as ex:
+        fused = list(ex.map(lambda i: keys.bootstrap_big(cts[i], tvs[i]), range(n)))
+        rad = list(ex.map(lambda i: radix.bootstrap_big(cts[i], tvs[i]), range(n)))
+
+    def err63(x):  # centred residue mod 2^63 (+-2^62 both decode to the same message bit)
+        x &= (1 << 63) - 1
+        return x - (1 << 63) if x >= 1 << 62 else x
+    want = [(int(f1[i]) if bits[i] else int(f0[i])) << 62 for i in range(n)]
+    ef = np.array([err63(keys.phase(fused[i]) - want[i]) for i in range(n)], dtype=float)
+    er = np.array([err63(keys.phase(rad[i]) - want[i]) for i in range(n)], dtype=float)
+    diff = np.array([_signed(keys.phase(a) - keys.phase(b)) for a, b in zip(fused, rad)], dtype=float)
+    assert np.abs(ef).max() < 2.0 ** 40 and np.abs(er).max() < 2.0 ** 40  # margin 2^61
+    assert np.abs(diff).max() < 2.0 ** 37, np.log2(np.abs(diff).max())
+    assert ef.var() <= 1.0 * er.var(), (ef.var() / er.var())
+
+
 def test_circuit_bootstrap_fused_vs_radix_lvl64(oracle_mod, oracle_keys, golden):
     """One 8 -> 24 WoP-PBS (SBOX + GF multiples with the gf quirk) per input, through both transforms."""
     keys = oracle_keys

@@ -63,7 +63,8 @@ class Engine {
     // homomorphic_shift_boolean at cbs level `level`: [B][n+1] -> [B][K+1]
     void pbs_shift_boolean(const uint64_t *d_small, uint64_t *d_big, size_t B, int level);
     // generic FourierLweBootstrapKey::bootstrap with LUT GLWEs [(k+1)N]: ciphertext b takes
-    // d_lut_glwe + (b % lut_mod) (k+1)N (lut_mod 1: one LUT for the batch; > 1 only on the generic kernel)
+    // d_lut_glwe + (b % lut_mod) (k+1)N (lut_mod 1: one LUT for the batch; lut_mod > 1, a test vector per
+    // ciphertext, runs on br512x4<7, true, 6> for shortint_1bit and on the generic pbs_kernel otherwise)
     void bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint64_t *d_big, size_t B,
                    uint64_t body_add, uint64_t out_add, size_t lut_mod = 1);
     // private functional keyswitches of level `level`: [B][K+1] -> GGSW rows of that level in

@@ -11,6 +11,8 @@
 //                         (fhe_sbox_gal_mul_pbs.rs:61-132, data_model.rs:270-281)
 #include <hip/hip_runtime.h>
 
+#include <cerrno>
+
 #include <algorithm>
 #include <cstdio>
 #include <climits>
@@ -1503,8 +1505,28 @@ void Engine::s1_multivariate(const uint64_t *d_bits, size_t G, int nbits, const 
     // Each selector level halves the batch; at 128 rows per CU the last level of an 8-bit tree still has a
     // bootstrap per CU (the AES S-box: 8 x 128 rows per group, 32 groups per chunk on 256 CUs, 2 GB).
     // TAE_S1_ROWS overrides the row budget (tests, A/B).
-    const char *rows_env = getenv("TAE_S1_ROWS");
-    const size_t rows = rows_env ? (size_t)atol(rows_env) : std::max<size_t>(kS1Rows, 128 * (size_t)num_cu_);
+    // The value must be a positive integer; anything else throws.  The budget is clamped so that the chunk's
+    // scratch fits in half of the free device memory.
+    size_t rows = std::max<size_t>(kS1Rows, 128 * (size_t)num_cu_);
+    if (const char *rows_env = getenv("TAE_S1_ROWS")) {
+        char *end = nullptr;
+        errno = 0;
+        const long long v = strtoll(rows_env, &end, 10);
+        if (errno != 0 || end == rows_env || *end != '\0' || v <= 0)
+            throw std::runtime_error(std::string("TAE_S1_ROWS must be a positive integer, got '") + rows_env + "'");
+        rows = (size_t)v;
+    }
+    {
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0) {
+            // per level-0 row: gathered input and output shortints, a packing-keyswitch GLWE, half a test vector,
+            // and the bootstrap's big-LWE output
+            const size_t per_row = sizeof(uint64_t) * (2 * p_.small_len() + p_.glwe_len() + p_.glwe_len() / 2 +
+                                                       (size_t)p_.k * p_.N + 1);
+            const size_t cap = std::max<size_t>(1, free_b / 2 / per_row);
+            rows = std::min(rows, cap);
+        }
+    }
     const size_t rows_per_group = (size_t)n_fn << (nbits - 1);
     const size_t gc = std::max<size_t>(1, rows / rows_per_group);
     const size_t L = p_.small_len();
