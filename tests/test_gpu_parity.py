@@ -70,12 +70,15 @@ def test_pbs_shift_boolean_bit_exact(gpu_context, oracle_keys, bits_cts):
         assert min(err, (1 << 64) - err) < 1 << 45
 
 
-@pytest.mark.parametrize("kernel", ["br512lat", "br512x4"])
+@pytest.mark.parametrize("kernel", ["br512lat", "br512x4", "br512p16"])
 def test_pbs_kernels_bit_exact(product_raw, oracle_keys, bits_cts, kernel, monkeypatch):
-    """Both N=512 blind rotations on the same 7 ciphertexts: the small-batch latency kernel (one
-    ciphertext per workgroup, levels in parallel) and the throughput kernel (three per workgroup,
-    forced with TAE_BR_LAT_MAX=0), each equal to the oracle word for word."""
+    """Every N=512 blind rotation on the same 7 ciphertexts: the small-batch latency kernel (one
+    ciphertext per workgroup, levels in parallel) and the two throughput kernels (forced with
+    TAE_BR_LAT_MAX=0; TAE_PBS_KERNEL picks br512x4, three ciphertexts per workgroup, or br512p16, two per
+    workgroup with sixteen points per lane, the last workgroup holding one), each equal to the oracle word
+    for word."""
     monkeypatch.setenv("TAE_BR_LAT_MAX", "256" if kernel == "br512lat" else "0")
+    monkeypatch.setenv("TAE_PBS_KERNEL", "p16" if kernel == "br512p16" else "x4")
     ctx = tfhe_aes.context_from_raw(tfhe_aes.PARAMS_SQRD_LVL_64, product_raw[1], device=0)
     bits, cts = bits_cts
     n = 7
@@ -86,17 +89,22 @@ def test_pbs_kernels_bit_exact(product_raw, oracle_keys, bits_cts, kernel, monke
         assert np.array_equal(out[i], oracle_keys.homomorphic_shift_boolean(small[i], 1)), i
 
 
-def test_pbs_split_batch_bit_exact(gpu_context, oracle_keys, client):
-    """A batch of 3 x 256 + 5 ciphertexts: whole rounds on br512x4, the 5-ciphertext remainder on
-    br512lat (Engine::bootstrap); ciphertexts from both parts equal the oracle's."""
-    B = 3 * 256 + 5
+@pytest.mark.parametrize("kernel", ["x4", "p16"])
+def test_pbs_split_batch_bit_exact(product_raw, oracle_keys, client, kernel, monkeypatch):
+    """A batch of C x 256 + 5 ciphertexts (C = 3 for br512x4, 2 for br512p16): whole rounds on the throughput
+    kernel, the 5-ciphertext remainder on br512lat (Engine::bootstrap); ciphertexts from both parts equal
+    the oracle's."""
+    monkeypatch.setenv("TAE_PBS_KERNEL", kernel)
+    gpu_context = tfhe_aes.context_from_raw(tfhe_aes.PARAMS_SQRD_LVL_64, product_raw[1], device=0)
+    cpw = 3 if kernel == "x4" else 2
+    B = cpw * 256 + 5
     bits = np.random.default_rng(7).integers(0, 2, size=B).astype(np.uint8)
     cts = client.encrypt_bits_raw(bits, start_index=40_000)
     small = np.zeros((B, SMALL), dtype=np.uint64)
     _stage(N.lib().tae_stage_keyswitch, gpu_context._h, _vp(cts), B, _vp(small), N.TAE_MEM_HOST)
     out = np.zeros((B, BIG), dtype=np.uint64)
     _stage(N.lib().tae_stage_pbs_shift_boolean, gpu_context._h, _vp(small), B, 1, _vp(out), N.TAE_MEM_HOST)
-    for i in (0, 767, 768, B - 1):
+    for i in (0, 1, cpw * 256 - 1, cpw * 256, B - 1):
         assert np.array_equal(out[i], oracle_keys.homomorphic_shift_boolean(small[i], 1)), i
 
 

@@ -233,6 +233,8 @@ class Engine {
     bool lf512_ = false;      // N = 512, k = 4: the fused transform, conj(E2)-rescaled BSK (oracle lf_set)
     bool x4_s1_ = false;      // shortint_1bit PBS 7 x 2^6: br512x4<7, true, 6> with per-ciphertext test vectors
     long lat_max_ = 256;      // batch size up to which br512lat runs (TAE_BR_LAT_MAX)
+    bool p16_ = false;        // lvl_64 PBS batches on br512p16 (two ciphertexts per workgroup) instead of br512x4
+                              // (TAE_PBS_KERNEL = p16 / x4)
     int num_cu_ = 256;
     double *d_lf_ = nullptr;  // the fused-twiddle transform's table (lf512.hpp: params_sqrd_lvl_64, lf1k.hpp: 8-bit)
     bool timing_ = false, clock_ = false;

@@ -22,6 +22,7 @@
 #include "aes.hpp"
 #include "br512.hpp"
 #include "br512x4.hpp"
+#include "br512p16.hpp"
 #include "br512lat.hpp"
 #include "br1024.hpp"
 #include "br1024lat.hpp"
@@ -772,7 +773,16 @@ void Engine::init_common() {
     const char *blat = getenv("TAE_BR_LAT_MAX");
     lat_max_ = blat ? atol(blat) : 256;
     HIPC(hipDeviceGetAttribute(&num_cu_, hipDeviceAttributeMultiprocessorCount, device_));
+    // the lvl_64 PBS throughput kernel: br512p16 (sixteen points per lane, two ciphertexts per workgroup) or
+    // br512x4 (four points per lane, three per workgroup); TAE_PBS_KERNEL = p16 / x4 (A/B knob, both pinned by tests)
+    if (const char *pk = getenv("TAE_PBS_KERNEL")) {
+        if (!strcmp(pk, "p16")) p16_ = true;
+        else if (!strcmp(pk, "x4")) p16_ = false;
+        else throw std::runtime_error(std::string("TAE_PBS_KERNEL must be p16 or x4, got '") + pk + "'");
+    }
     if (x4_512_) {
+        HIPC(hipFuncSetAttribute((const void *)br512p16::br_kernel<3, 12>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)br512p16::lds_bytes()));
         HIPC(hipFuncSetAttribute((const void *)br512lat::br_kernel<3, 12>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)br512lat::lds_bytes(3)));
         HIPC(hipFuncSetAttribute((const void *)br512x4::br_kernel<3, true, 12>,
@@ -1040,16 +1050,21 @@ void Engine::bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint
             HIPC(hipGetLastError());
             return;
         }
-        // whole rounds of three ciphertexts per CU on br512x4; a remainder that would leave most
-        // CUs idle in a last round goes to br512lat (one ciphertext per CU, ~0.6x the round time)
+        // whole rounds of C ciphertexts per CU on the throughput kernel (br512p16: C = 2, br512x4: C = 3); a
+        // remainder that would leave most CUs idle in a last round goes to br512lat (one ciphertext per CU)
         long bx = (long)B;
-        const long per_round = 3L * num_cu_, rest = (long)B % per_round;
+        const long cpw = p16_ ? br512p16::C : br512x4::C;
+        const long per_round = cpw * num_cu_, rest = (long)B % per_round;
         if ((long)B > per_round && rest > 0 && rest <= std::min<long>(lat_max_, num_cu_)) bx -= rest;
-        const unsigned wgs = (unsigned)((bx + 2) / 3);
+        const unsigned wgs = (unsigned)((bx + cpw - 1) / cpw);
         uint64_t *clk = clock_buffer(wgs);
         timed(ST_PBS_MAIN, [&] {
-            br512x4::br_kernel<3, true, 12><<<wgs, br512x4::THREADS, br512x4::lds_bytes(), stream_>>>(
-                d_small, p_.n, d_lut_glwe, 0, d_bsk_f_, 0, d_big, bx, body_add, out_add, d_twist_, d_w_, d_lf_, clk);
+            if (p16_)
+                br512p16::br_kernel<3, 12><<<wgs, br512p16::THREADS, br512p16::lds_bytes(), stream_>>>(
+                    d_small, p_.n, d_lut_glwe, d_bsk_f_, d_big, bx, body_add, out_add, d_lf_, clk);
+            else
+                br512x4::br_kernel<3, true, 12><<<wgs, br512x4::THREADS, br512x4::lds_bytes(), stream_>>>(
+                    d_small, p_.n, d_lut_glwe, 0, d_bsk_f_, 0, d_big, bx, body_add, out_add, d_twist_, d_w_, d_lf_, clk);
             HIPC(hipGetLastError());
         });
         record_clock(clk, wgs);
