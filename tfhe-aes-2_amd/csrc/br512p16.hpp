@@ -68,6 +68,29 @@ __host__ __device__ constexpr int inv_off(int k) { return (k >> 1) * GROUP_BYTES
 
 using lf512::K4;
 
+// TAE_P16_PROF (debug builds only, never the product): per-phase cycle sums (clock64) of every wave of one
+// workgroup, printed at exit: 0 decomposition, 1 barrier after it, 2 forward transforms, 3 GGSW prefetch +
+// barrier, 4 MAC, 5 barrier after it, 6 accumulator stores + barrier, 7 inverse + ACC update.
+#ifdef TAE_P16_PROF
+#define P16_PROF_ARGS , uint64_t *prof_, uint64_t &prof_t_
+#define P16_PROF_PASS , prof_, prof_t_
+#define P16_PROF_DECL uint64_t prof_[8] = {0}, prof_t_ = clock64();
+#define P16_T(i)                         \
+    do {                                 \
+        asm volatile("" ::: "memory");   \
+        const uint64_t now_ = clock64(); \
+        prof_[i] += now_ - prof_t_;      \
+        prof_t_ = now_;                  \
+    } while (0)
+#else
+#define P16_PROF_ARGS
+#define P16_PROF_PASS
+#define P16_PROF_DECL
+#define P16_T(i) \
+    do {         \
+    } while (0)
+#endif
+
 // MAC thread groups (waves 4 G .. 4 G + 3, one per SIMD): accumulators (q, ct) for both ct and q = QA, plus q = 4
 // in group 2 (NQ = 2), so that each GGSW value is loaded once per workgroup: 2 / 2 / 4 / 2 accumulators.
 template <int G>
@@ -122,12 +145,13 @@ __device__ __forceinline__ void mac_level(const unsigned char *mrow, int lev, co
 // barriers on every path.
 template <int G>
 __device__ __forceinline__ void mac_step(unsigned char *jarea, int mslot, int spos, __amdgpu_buffer_rsrc_t grs,
-                                         int gvoff, int gstep) {
+                                         int gvoff, int gstep P16_PROF_ARGS) {
     constexpr int NQ = MacGroup<G>::NQ;
     cplx g3[K1 * NQ], g2[K1 * NQ], g1[K1 * NQ], accr[NQ * C];
     mac_load<G>(g3, 3, grs, gvoff, gstep);
     mac_load<G>(g2, 2, grs, gvoff, gstep);
     lds_sync();
+    P16_T(3);
     const unsigned char *mrow = jarea + mslot * 16;
 #pragma unroll
     for (int a = 0; a < NQ * C; a++) accr[a] = cplx{0.0, 0.0};
@@ -135,13 +159,16 @@ __device__ __forceinline__ void mac_step(unsigned char *jarea, int mslot, int sp
     mac_load<G>(g1, 1, grs, gvoff, gstep);
     mac_level<G>(mrow, 2, g2, accr);
     mac_level<G>(mrow, 1, g1, accr);
+    P16_T(4);
     lds_sync();
+    P16_T(5);
 #pragma unroll
     for (int qi = 0; qi < NQ; qi++)
 #pragma unroll
         for (int ct = 0; ct < C; ct++)
             *reinterpret_cast<cplx *>(jarea + inv_off(ct * K1 + MacGroup<G>::q(qi)) + spos * 16) = accr[qi * C + ct];
     lds_sync();
+    P16_T(6);
 }
 
 // PBS: lwe_in [B][n+1] (small key), lut the test vector GLWE [(k+1) N], bsk the Fourier BSK (conj(E2)-rescaled),
@@ -204,6 +231,7 @@ __global__ void __launch_bounds__(THREADS, 1)
     const int baseB = br512x4::SF[4 * r + (u & 3)] + br512x4::SG3[u >> 2];
 
     uint64_t a_next = (iw && ict < nct) ? lwe_in[(size_t)(ct0 + ict) * (n + 1)] : 0;
+    P16_PROF_DECL
     for (int step = 0; step < n; step++) {
         const int gstep = step * (int)(ggsw_sz * sizeof(cplx));
         // ---- D: rotated difference and digits of polynomial kp, all levels -> digit slots ----
@@ -238,7 +266,9 @@ __global__ void __launch_bounds__(THREADS, 1)
                 *reinterpret_cast<u32x4 *>(jarea + dig_off(kp * LEV + l) + (16 * r + u) * 16) = w;
             }
         }
+        P16_T(0);
         lds_sync();
+        P16_T(1);
         // ---- F: forward transforms, 16 points per lane ----
         if (fvalid) {
             const unsigned char *ds = jarea + dig_off(fjob);
@@ -291,12 +321,13 @@ __global__ void __launch_bounds__(THREADS, 1)
                     *reinterpret_cast<cplx *>(smem + (Bk ^ (16 * (l1 + 4 * k2)))) = v[k2];
             }
         }
+        P16_T(2);
         // ---- M: the external product's MAC (three barriers) ----
         switch (grp) {
-        case 0: mac_step<0>(jarea, mslot, spos, grs, gvoff, gstep); break;
-        case 1: mac_step<1>(jarea, mslot, spos, grs, gvoff, gstep); break;
-        case 2: mac_step<2>(jarea, mslot, spos, grs, gvoff, gstep); break;
-        default: mac_step<3>(jarea, mslot, spos, grs, gvoff, gstep); break;
+        case 0: mac_step<0>(jarea, mslot, spos, grs, gvoff, gstep P16_PROF_PASS); break;
+        case 1: mac_step<1>(jarea, mslot, spos, grs, gvoff, gstep P16_PROF_PASS); break;
+        case 2: mac_step<2>(jarea, mslot, spos, grs, gvoff, gstep P16_PROF_PASS); break;
+        default: mac_step<3>(jarea, mslot, spos, grs, gvoff, gstep P16_PROF_PASS); break;
         }
         // ---- I: inverse transform of (ct, q) = kp, accumulated into its ACC polynomial ----
         if (iw) {
@@ -339,7 +370,18 @@ __global__ void __launch_bounds__(THREADS, 1)
             }
             wave_sync();  // the next step's decomposition (this wave) reads these ACC writes (in-order LDS)
         }
+#ifdef TAE_P16_PROF
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+        P16_T(7);
     }
+#ifdef TAE_P16_PROF
+    if (blockIdx.x == 100 && lane == 0)
+        printf("p16prof wave %2d: dec %llu barD %llu fwd %llu pre+barF %llu mac %llu barM %llu store %llu inv %llu\n", wv,
+               (unsigned long long)prof_[0], (unsigned long long)prof_[1], (unsigned long long)prof_[2],
+               (unsigned long long)prof_[3], (unsigned long long)prof_[4], (unsigned long long)prof_[5],
+               (unsigned long long)prof_[6], (unsigned long long)prof_[7]);
+#endif
     lds_sync();  // sample extraction reads every polynomial's ACC
     for (int ct = 0; ct < nct; ct++) {
         const uint64_t *a = acc + ct * K1 * N;
