@@ -675,7 +675,27 @@ T *Engine::grow(T *&ptr, size_t &cap, size_t count) {
 
 void Engine::init_common() {
     HIPC(hipSetDevice(device_));
-    HIPC(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    // TAE_CU_MASK (probe / A-B knob, scripts/probes/stage_overlap.py): "lo:N" or "hi:N" restricts the engine
+    // stream to the first / last N CUs of the device's CU mask (hipExtStreamCreateWithCUMask); batch rounds
+    // are then sized for N CUs
+    int mask_cus = 0;
+    if (const char *cm = getenv("TAE_CU_MASK")) {
+        int total = 0;
+        HIPC(hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, device_));
+        const bool hi = !strncmp(cm, "hi:", 3);
+        if (!hi && strncmp(cm, "lo:", 3)) throw std::runtime_error("TAE_CU_MASK must be lo:N or hi:N");
+        const int nc = atoi(cm + 3);
+        if (nc < 1 || nc > total || total > 256) throw std::runtime_error("TAE_CU_MASK: bad CU count");
+        uint32_t mask[8] = {0};
+        for (int c = 0; c < nc; c++) {
+            const int b = hi ? total - 1 - c : c;
+            mask[b >> 5] |= 1u << (b & 31);
+        }
+        HIPC(hipExtStreamCreateWithCUMask(&stream_, 8, mask));
+        mask_cus = nc;
+    } else {
+        HIPC(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    }
     if (p_.N != 512 && p_.N != 1024) throw std::runtime_error("unsupported polynomial size");
     const FftTables t = make_fft_tables(p_.N);
     const size_t tb = sizeof(double) * 2 * t.M;
@@ -773,6 +793,7 @@ void Engine::init_common() {
     const char *blat = getenv("TAE_BR_LAT_MAX");
     lat_max_ = blat ? atol(blat) : 256;
     HIPC(hipDeviceGetAttribute(&num_cu_, hipDeviceAttributeMultiprocessorCount, device_));
+    if (mask_cus) num_cu_ = mask_cus;
     // the lvl_64 PBS throughput kernel: br512p16 (sixteen points per lane, two ciphertexts per workgroup) or
     // br512x4 (four points per lane, three per workgroup); TAE_PBS_KERNEL = p16 / x4 (A/B knob, both pinned by tests)
     if (const char *pk = getenv("TAE_PBS_KERNEL")) {
