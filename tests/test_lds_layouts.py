@@ -56,3 +56,22 @@ def test_br1024_separable_tables_cannot_be_conflict_free(tmp_path):
                    check=True)
     out = subprocess.run([exe], capture_output=True, text=True, timeout=300).stdout
     assert "found 0" in out
+
+
+def test_fft_torus_1024_final_reads_conflict_free():
+    import fft1k_banks
+    src = _header("kernels.hip")
+    assert _table(src, "kFftTau1k") == fft1k_banks.tau()
+    t = fft1k_banks.tau()
+    fs = sorted(128 * (c >> 1) + 32 * (c & 1) + t[u] for c in range(8) for u in range(64))
+    assert fs == list(range(512))  # every output once
+    # each read instruction stores whole 128-byte lines (8 complex values)
+    for c in range(8):
+        blocks = {}
+        for u in range(64):
+            f = 128 * (c >> 1) + 32 * (c & 1) + t[u]
+            blocks.setdefault(f >> 3, set()).add(f & 7)
+        assert all(len(v) == 8 for v in blocks.values())
+    ex = fft1k_banks.extra_cycles()
+    assert ex["final_read_lane_order"] > 0
+    assert all(v == 0 for k, v in ex.items() if k != "final_read_lane_order"), ex

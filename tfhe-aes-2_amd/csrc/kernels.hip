@@ -304,6 +304,11 @@ template <int M>
 __device__ __forceinline__ int fft_pidx(int f) { return M == 256 ? f + (f >> 4) : f + (f >> 3); }
 template <int M>
 constexpr int fft_poly_stride() { return M == 256 ? 272 : M + M / 8; }
+// lane -> offset inside a pair of 64-value output chunks for the N = 1024 final reads (see fft_torus_kernel)
+__constant__ unsigned char kFftTau1k[64] = {0,  1,  2,  3,  8,  9,  10, 11, 12, 13, 14, 15, 4,  5,  6,  7,
+                                            72, 73, 74, 75, 64, 65, 66, 67, 68, 69, 70, 71, 76, 77, 78, 79,
+                                            16, 17, 18, 19, 24, 25, 26, 27, 28, 29, 30, 31, 20, 21, 22, 23,
+                                            88, 89, 90, 91, 80, 81, 82, 83, 84, 85, 86, 87, 92, 93, 94, 95};
 
 template <int N>
 __global__ void __launch_bounds__(kThreads) fft_torus_kernel(const uint64_t *__restrict__ in, cplx *__restrict__ out,
@@ -351,7 +356,19 @@ __global__ void __launch_bounds__(kThreads) fft_torus_kernel(const uint64_t *__r
     }
     if (active) {
         cplx *dst = out + poly * M;
-        for (int f = u; f < M; f += TPJ) dst[f] = X[fft_pidx<M>(f)];
+        if constexpr (M == 512) {
+            // final reads of N = 1024 by lane permutation: read c (0..7) of lane u takes f = 128 (c >> 1) + 32 (c & 1)
+            // + kFftTau1k[u], which gives each ds_read_b128 lane group the two 8-blocks a, a + 8 of f, whose slots
+            // 9 a + b cover all 16 bank groups (the lane-ordered f = u + 64 c were 2-way conflicts in every group;
+            // scripts/layout/fft1k_banks.py); every read still stores whole 128-byte lines
+#pragma unroll
+            for (int c = 0; c < 8; c++) {
+                const int f = 128 * (c >> 1) + 32 * (c & 1) + kFftTau1k[u];
+                dst[f] = X[fft_pidx<M>(f)];
+            }
+        } else {
+            for (int f = u; f < M; f += TPJ) dst[f] = X[fft_pidx<M>(f)];
+        }
     }
 }
 

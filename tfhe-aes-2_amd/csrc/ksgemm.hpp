@@ -474,6 +474,7 @@ __global__ void __launch_bounds__(256 * WM, 1)
     const long N8 = (long)ncols * 8;
 
     const int lrow = lane >> 2, lch = lane & 3;
+    const int nk = Kp / G4K;
     auto stage = [&](int st, int ks) {
         const int k0 = ks * G4K;
         int8_t *base = smem_g + st * SAB;
@@ -491,7 +492,35 @@ __global__ void __launch_bounds__(256 * WM, 1)
             g4_glds(src, base + 16 * p * G4K);
         }
     };
+#ifdef TAE_G6_PF
+    // L2 prefetch TAE_G6_PF steps beyond the ring (A/B knob): before each step's stage DMA, wave 0 loads one
+    // dword of 56 operand lines of step ks + G4S - 1 + TAE_G6_PF (this tile's share of the lines its XCD's
+    // co-resident tiles stream: A lines (nt mod 8) x 24 .. + 23 of its 192, B lines (mt mod 4) x 32 .. + 31 of its
+    // 128) into the first 256 bytes of the stage that its own DMA then overwrites (vector-memory returns are
+    // in issue order), so the ring's loads of that step find their lines in L2.
+    const bool pf_wave = wave == 0;
+    auto prefetch = [&](int st, int ks) {
+        if (!pf_wave) return;
+        const int kp = min(ks, nk - 1) * G4K;
+        const int8_t *src;
+        if (lane < 24 || lane >= 56) {
+            const int a = (int)(nt & 7) * 24 + (lane < 24 ? lane : lane - 56);
+            src = A + op_off(row0 + 2 * a, kp, Kp, true);
+        } else {
+            const int b = (int)(mt & 3) * 32 + lane - 24;
+            src = Bt + op_off(min(col8_0 + 2 * b, N8 - 2), kp, Kp, true);
+        }
+#if defined(__HIP_DEVICE_COMPILE__)
+        __builtin_amdgcn_global_load_lds(src, smem_g + st * SAB, 4, 0, 0);
+#else
+        (void)src;
+        (void)st;
+#endif
+    };
+    const int per_wave = (NP / NW) + (wave < NP % NW ? 1 : 0) + (pf_wave ? 1 : 0);
+#else
     const int per_wave = (NP / NW) + (wave < NP % NW ? 1 : 0);
+#endif
     auto wait_steps = [&](int keep) {  // retire all but this wave's loads of `keep` later steps
         switch (per_wave * keep) {
         case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
@@ -512,8 +541,12 @@ __global__ void __launch_bounds__(256 * WM, 1)
         for (int b = 0; b < 2; b++) acc[a][b] = v16i{0};
 
     const int r = lane & 31, h = lane >> 5;
-    const int nk = Kp / G4K;
-    for (int ks = 0; ks < G4S - 1 && ks < nk; ks++) stage(ks, ks);
+    for (int ks = 0; ks < G4S - 1 && ks < nk; ks++) {
+#ifdef TAE_G6_PF
+        prefetch(ks, ks + G4S - 1 + TAE_G6_PF);
+#endif
+        stage(ks, ks);
+    }
     for (int ks = 0; ks < nk; ks++) {
         wait_steps(min(G4S - 2, nk - 1 - ks));
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -522,7 +555,12 @@ __global__ void __launch_bounds__(256 * WM, 1)
 #endif
         __builtin_amdgcn_sched_barrier(0);
 #ifndef TAE_G6_NODMA  // timing-only bound (stale tiles): no operand stream after the prologue
-        if (ks + G4S - 1 < nk) stage((ks + G4S - 1) % G4S, ks + G4S - 1);
+        if (ks + G4S - 1 < nk) {
+#ifdef TAE_G6_PF
+            prefetch((ks + G4S - 1) % G4S, ks + 2 * (G4S - 1) + TAE_G6_PF);
+#endif
+            stage((ks + G4S - 1) % G4S, ks + G4S - 1);
+        }
 #endif
         const int8_t *a_s = smem_g + (ks % G4S) * SAB, *b_s = a_s + SA;
         v4i fa[2][3], fb[2][2];
