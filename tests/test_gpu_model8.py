@@ -58,15 +58,19 @@ def test_pbs_shift_boolean8_bit_exact(gpu_context8, oracle_keys8, client8, level
         assert min(err, (1 << 64) - err) < 1 << (63 - 6 * level), (i, level)  # within alpha
 
 
-@pytest.mark.parametrize("lat,pair,B,occ2", [("1", "1", 5, "0"), ("0", "1", 5, "0"), ("0", "0", 5, "0"),
-                                             ("1", "1", 300, "0"), ("1", "1", 513, "0"), ("1", "1", 513, "1")])
-def test_pbs8_kernel_variants_bit_exact(product_raw8, oracle_keys8, client8, lat, pair, B, occ2):
+@pytest.mark.parametrize("lat,pair,B,occ2,wide", [("1", "1", 5, "0", "1"), ("0", "1", 5, "0", "1"),
+                                                  ("0", "0", 5, "0", "1"), ("1", "1", 300, "0", "1"),
+                                                  ("1", "1", 513, "0", "1"), ("1", "1", 513, "1", "1"),
+                                                  ("1", "1", 1027, "0", "1"), ("1", "1", 1027, "0", "0")])
+def test_pbs8_kernel_variants_bit_exact(product_raw8, oracle_keys8, client8, lat, pair, B, occ2, wide):
     """The N=1024 blind-rotation variants the engine picks, all on the fused-twiddle transform (lf1k.hpp,
     the oracle's or_lf1k_*): for batches up to one ciphertext per CU the 1024-thread latency kernel
     (br1024lat, default), or with TAE_B1K_LAT=0 br1024 with one ciphertext per workgroup and two levels
     per pass (or one: TAE_B1K_PAIR=0); and two ciphertexts per workgroup (B > the CU count, odd tail
-    workgroup of one); TAE_B1K_OCC2=1: large batches as one ciphertext per workgroup, two per CU."""
-    env = {"TAE_B1K_LAT": lat, "TAE_B1K_PAIR": pair, "TAE_B1K_OCC2": occ2}
+    workgroup of one); TAE_B1K_OCC2=1: large batches as one ciphertext per workgroup, two per CU; from four
+    ciphertexts per CU on br1024w, four per workgroup with the ACC stash (B = 1027: a ragged last workgroup of
+    three; TAE_B1K_WIDE=0: br1024 with two per workgroup instead)."""
+    env = {"TAE_B1K_LAT": lat, "TAE_B1K_PAIR": pair, "TAE_B1K_OCC2": occ2, "TAE_B1K_WIDE": wide}
     os.environ.update(env)
     try:
         ctx = tfhe_aes.context_from_raw(tfhe_aes.PARAMS_WOPPBS_8BIT, product_raw8[1], device=0)
@@ -77,7 +81,7 @@ def test_pbs8_kernel_variants_bit_exact(product_raw8, oracle_keys8, client8, lat
     small = client8.encrypt_bits_raw(bits, start_index=900)
     out = np.zeros((B, BIG), dtype=np.uint64)
     _stage(N.lib().tae_stage_pbs_shift_boolean, ctx._h, _vp(small), B, 2, _vp(out), N.TAE_MEM_HOST)
-    for i in sorted({0, B // 2, B - 1}):
+    for i in sorted({0, min(3, B - 1), B // 2, B - 1}):
         assert np.array_equal(out[i], oracle_keys8.homomorphic_shift_boolean(small[i], 2)), i
     del ctx
 

@@ -4,3 +4,10 @@
 
 #define TAE_B1K_INSTANTIATE
 #include "br1024.hpp"
+#include "br1024w.hpp"
+
+namespace tae {
+namespace br1024w {
+template __global__ void br_kernel<6, 7>(TAE_B1KW_PARAMS);
+}  // namespace br1024w
+}  // namespace tae

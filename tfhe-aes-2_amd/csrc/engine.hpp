@@ -224,6 +224,9 @@ class Engine {
     decltype(br1024_pbs_) br1024_occ2_ = nullptr;  // A/B: one per workgroup, two workgroups per CU
     int br1024_pbs1_lp_ = 1;                       // its levels per pass
     bool lf1k_ = false;                            // the 8-bit model's PBS: the N = 1024 fused transform (lf1k.hpp)
+    bool b1kw_ = false;                            // ... on br1024w (four ciphertexts per workgroup, ACC stash)
+    uint64_t *d_acc_w_ = nullptr;                  // br1024w's ACC stash [B][k+1][N]
+    size_t cap_acc_w_ = 0;
     // latency blind rotation, one ciphertext per 1024-thread workgroup (br1024lat.hpp), or nullptr
     void (*br1024lat_)(const uint64_t *, int, const uint64_t *, const cplx *, uint64_t *, long, uint64_t, uint64_t,
                        const cplx *, const double *) = nullptr;

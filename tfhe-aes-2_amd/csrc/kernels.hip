@@ -25,6 +25,7 @@
 #include "br512p16.hpp"
 #include "br512lat.hpp"
 #include "br1024.hpp"
+#include "br1024w.hpp"
 #include "br1024lat.hpp"
 #include "ksgemm.hpp"
 #include "engine.hpp"
@@ -856,6 +857,13 @@ void Engine::init_common() {
             if (kf)
                 HIPC(hipFuncSetAttribute((const void *)kf, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          (int)br1024::lds_bytes(2)));
+        // the 8-bit model's PBS at large batches: four ciphertexts per 768-thread workgroup (br1024w.hpp;
+        // TAE_B1K_WIDE=0: br1024's two-ciphertext kernel instead)
+        const char *wide = getenv("TAE_B1K_WIDE");
+        b1kw_ = lf1k_ && p_.pbs_l == 6 && p_.pbs_b == 7 && !(wide && wide[0] == '0');
+        if (b1kw_)
+            HIPC(hipFuncSetAttribute((const void *)br1024w::br_kernel<6, 7>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)br1024w::lds_bytes()));
         // one ciphertext per 1024-thread workgroup, three levels per pass (the 8-bit model's PBS;
         // TAE_B1K_LAT=0: br1024's one-ciphertext kernel instead)
         const char *blat = getenv("TAE_B1K_LAT");
@@ -1017,7 +1025,7 @@ Engine::~Engine() {
                     (void *)d_ggsw_f_, (void *)d_state_, (void *)d_muls_, (void *)d_pf_bt_, (void *)d_ks_bt_, (void *)d_pf_corr_, (void *)d_pf_bt_kl_,
                     (void *)d_digits_, (void *)d_wlut_sbox_, (void *)d_wlut_id_, (void *)d_lut_x_, (void *)d_xbuf_,
                     (void *)d_xsh_, (void *)d_xks_, (void *)d_xpbs_, (void *)d_ints_, (void *)d_s1_sbox_tv_,
-                    (void *)d_s1_id_tv_, (void *)d_s1_in_, (void *)d_s1_out_, (void *)d_s1_pks_, (void *)d_s1_tv_, (void *)d_pf_flags_, (void *)d_clk_, (void *)d_lf_})
+                    (void *)d_s1_id_tv_, (void *)d_s1_in_, (void *)d_s1_out_, (void *)d_s1_pks_, (void *)d_s1_tv_, (void *)d_pf_flags_, (void *)d_clk_, (void *)d_lf_, (void *)d_acc_w_})
         if (q) hipFree(q);
     for (auto &e : ev_pool_) hipEventDestroy(e);
     if (caller_ev_) hipEventDestroy(caller_ev_);
@@ -1128,6 +1136,17 @@ void Engine::bootstrap(const uint64_t *d_small, const uint64_t *d_lut_glwe, uint
             d_lf_, clk);
         HIPC(hipGetLastError());
         record_clock(clk, B);
+        return;
+    }
+    if (b1kw_ && lut_mod == 1 && (long)B >= (long)br1024w::C * num_cu_) {
+        // four ciphertexts per workgroup (every CU busy from 4 x CUs ciphertexts on)
+        const size_t wgs = (B + br1024w::C - 1) / br1024w::C;
+        grow(d_acc_w_, cap_acc_w_, B * (size_t)(p_.k + 1) * p_.N);
+        uint64_t *clk = clock_buffer(wgs);
+        br1024w::br_kernel<6, 7><<<(unsigned)wgs, br1024w::THREADS, br1024w::lds_bytes(), stream_>>>(
+            d_small, p_.n, d_lut_glwe, d_bsk_f_, d_big, (long)B, body_add, out_add, d_w_, d_lf_, d_acc_w_, clk);
+        HIPC(hipGetLastError());
+        record_clock(clk, wgs);
         return;
     }
     if (br1024_pbs_) {
