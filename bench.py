@@ -33,7 +33,7 @@ HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (= FP64 matrix) dense peak, spec
 SPEC_CLOCK_GHZ = 2.4      # the clock the spec peaks assume
 FP64_SUSTAINED_TFLOPS = 58.0  # measured sustained v_fma_f64 rate, all CUs (scripts/probes/fp64_peak.hip)
-PBS_KERNELS = {"1bit": "tae::br512x4::br_kernel<3, true, 12>", "8bit": "tae::br1024::br_kernel<6, true, 7, 2, 1, 1>"}
+PBS_KERNELS = {"1bit": "tae::br512x4::br_kernel<3, true, 12>", "8bit": "tae::br1024w::br_kernel<6, 7>"}
 
 
 def pbs_algorithmic(p, bits):

@@ -31,6 +31,32 @@ using br1024::pidx;
 using br1024::s_setprio_c;
 using br1024::wave_sync;
 
+// TAE_B1KW_PROF (debug builds only, never the product): per-phase cycle sums of every wave of one workgroup,
+// printed at exit: 0 decomposition, 1 forward transforms, 2 barrier after them, 3 MAC, 4 barrier after it,
+// 5 MAC stores + barrier, 6 inverse + ACC update
+#ifdef TAE_B1KW_PROF
+#define WPROF_DECL uint64_t wprof_[7] = {0}, wprof_t_ = clock64();
+#define WPROF(i)                         \
+    do {                                 \
+        asm volatile("" ::: "memory");   \
+        const uint64_t now_ = clock64(); \
+        wprof_[i] += now_ - wprof_t_;    \
+        wprof_t_ = now_;                 \
+    } while (0)
+#else
+#define WPROF_DECL
+#define WPROF(i) \
+    do {         \
+    } while (0)
+#endif
+
+// TAE_B1KW_PRIO2 (A/B knob): a priority step-down after every FFT pass instead of br1024's schedule
+#ifdef TAE_B1KW_PRIO2
+#define B1KW_PRIO(a, b) s_setprio_c<(b)>()
+#else
+#define B1KW_PRIO(a, b) s_setprio_c<(a)>()
+#endif
+
 constexpr int C = 4, CJ = C * K1, THREADS = 64 * CJ;
 static_assert(THREADS == 3 * 256, "one wave per FFT job; the MAC: 256 threads per GGSW column");
 
@@ -95,6 +121,7 @@ __global__ void __launch_bounds__(THREADS, 3)
     uint64_t a_next = jvalid ? lwe_in[(size_t)(ct0 + jct) * (n + 1)] : 0;
     cplx accr[2 * C];  // [half h][ct]
     cplx gv[K1 * 2];   // [row p][half h]
+    WPROF_DECL
     for (int step = 0; step < n; step++) {
         s_setprio_c<2>();
         const uint64_t a = a_next;
@@ -126,6 +153,7 @@ __global__ void __launch_bounds__(THREADS, 3)
             }
         }
         wave_sync();  // the forward transform below overwrites the region the reads above came from
+        WPROF(0);
 #pragma unroll
         for (int a2 = 0; a2 < 2 * C; a2++) accr[a2] = cplx{0.0, 0.0};
 
@@ -140,6 +168,9 @@ __global__ void __launch_bounds__(THREADS, 3)
                         __builtin_amdgcn_raw_buffer_load_b128(grs, mpos[h] * (int)sizeof(cplx), soff, 0);
                     __builtin_memcpy(&gv[p * 2 + h], &rv, sizeof(cplx));
                 }
+#ifdef TAE_B1KW_PRIO2
+            s_setprio_c<3>();
+#endif
             {
                 cplx v[8];
                 // fused pass 0 (lf1k::pass0) of the level's digits -> position t + 64 kk
@@ -160,7 +191,11 @@ __global__ void __launch_bounds__(THREADS, 3)
 #pragma unroll
                 for (int kk = 0; kk < 8; kk++) X[pidx(tt + 64 * kk)] = v[kk];
                 wave_sync();
+#ifdef TAE_B1KW_PRIO2
+                s_setprio_c<2>();
+#else
                 if (lev == LEV) s_setprio_c<1>(); else s_setprio_c<2>();
+#endif
                 {  // pass 1: points 64 gg + uu + 8 m
                     const int gg = tt >> 3, uu = tt & 7;
 #pragma unroll
@@ -170,7 +205,11 @@ __global__ void __launch_bounds__(THREADS, 3)
                     for (int kk = 0; kk < 8; kk++) X[pidx(64 * gg + uu + 8 * kk)] = v[kk];
                 }
                 wave_sync();
+#ifdef TAE_B1KW_PRIO2
+                s_setprio_c<1>();
+#else
                 if (lev == LEV) s_setprio_c<0>(); else s_setprio_c<1>();
+#endif
                 // pass 2: points 8 t + m
 #pragma unroll
                 for (int m = 0; m < 8; m++) v[m] = X[pidx(8 * tt + m)];
@@ -178,7 +217,12 @@ __global__ void __launch_bounds__(THREADS, 3)
 #pragma unroll
                 for (int kk = 0; kk < 8; kk++) X[pidx(8 * tt + kk)] = v[kk];
             }
+            WPROF(1);
+#ifdef TAE_B1KW_PRIO2
+            s_setprio_c<0>();
+#endif
             br512::lds_sync();
+            WPROF(2);
             s_setprio_c<3>();
             // MAC: accumulator (mq, c) at position mpos[h] = accr[h * C + c]; rows p ascending.  The two slot
             // offsets are re-derived here (not 24 hoisted addresses held through the FFTs)
@@ -202,7 +246,9 @@ __global__ void __launch_bounds__(THREADS, 3)
                         accr[h * C + c] = {re, im};
                     }
                 }
+            WPROF(3);
             br512::lds_sync();
+            WPROF(4);
             s_setprio_c<3>();
         }
         // ---- inverse FFT of the MAC results, accumulated into the ACC ----
@@ -215,6 +261,7 @@ __global__ void __launch_bounds__(THREADS, 3)
                 for (int c = 0; c < C; c++) buf[(c * K1 + mq) * BUF_STRIDE + mslot[h]] = accr[h * C + c];
         }
         br512::lds_sync();
+        WPROF(5);
         s_setprio_c<3>();
         {
             // this lane's old ACC coefficients from the stash, issued first (their latency hides behind the passes)
@@ -237,6 +284,9 @@ __global__ void __launch_bounds__(THREADS, 3)
 #pragma unroll
             for (int m = 0; m < 8; m++) X[pidx(8 * tt + m)] = v[m];
             wave_sync();
+#ifdef TAE_B1KW_PRIO2
+            s_setprio_c<2>();
+#endif
             {  // inverse pass 1 (fused): points 64 gg + uu + 8 kk
                 const int gg = tt >> 3, uu = tt & 7;
 #pragma unroll
@@ -246,7 +296,7 @@ __global__ void __launch_bounds__(THREADS, 3)
                 for (int m = 0; m < 8; m++) X[pidx(64 * gg + uu + 8 * m)] = v[m];
             }
             wave_sync();
-            s_setprio_c<2>();
+            B1KW_PRIO(2, 1);
             // inverse pass 0 (fused): points t + 64 kk, then untwist by conj(twist) (the 2^-9 goes into the
             // torus conversion's exponent), from_torus, ACC +=
 #pragma unroll
@@ -272,7 +322,18 @@ __global__ void __launch_bounds__(THREADS, 3)
             }
         }
         wave_sync();  // the next decomposition (this wave) reads these LDS ACC writes (in-order LDS)
+#ifdef TAE_B1KW_PROF
+        asm volatile("s_waitcnt lgkmcnt(0) vmcnt(0)" ::: "memory");
+#endif
+        WPROF(6);
     }
+#ifdef TAE_B1KW_PROF
+    if (blockIdx.x == 100 && t == 0)
+        printf("b1kwprof wave %2d: dec %llu fwd %llu barF %llu mac %llu barM %llu store %llu inv %llu\n", jb,
+               (unsigned long long)wprof_[0], (unsigned long long)wprof_[1], (unsigned long long)wprof_[2],
+               (unsigned long long)wprof_[3], (unsigned long long)wprof_[4], (unsigned long long)wprof_[5],
+               (unsigned long long)wprof_[6]);
+#endif
     br512::lds_sync();  // sample extraction reads every job's LDS ACC
     for (int ct = 0; ct < nct; ct++) {
         uint64_t *o = out + (size_t)(ct0 + ct) * ((K1 - 1) * N + 1);
