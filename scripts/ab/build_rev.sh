@@ -14,7 +14,7 @@ mkdir -p dbg
   -c "$tmp/tfhe-aes-2_amd/csrc/kernels.hip" -o dbg/$name.o
 objs=dbg/$name.o
 # revisions with kernels in units of their own: each built with its Makefile flag variable
-for unit in br512x4_inst:X4FLAGS br512lat_inst:LATFLAGS br1024_inst:B1KFLAGS; do
+for unit in br512x4_inst:X4FLAGS br512lat_inst:LATFLAGS br1024_inst:B1KFLAGS br512p16_inst:P16FLAGS; do
   src=${unit%%:*}; var=${unit#*:}
   [ -f "$tmp/tfhe-aes-2_amd/csrc/$src.hip" ] || continue
   fl=$(git -C "$ROOT" show "$rev:tfhe-aes-2_amd/Makefile" | sed -n "s/^$var = //p")

@@ -158,6 +158,7 @@ __global__ void __launch_bounds__(THREADS, 3)
         for (int a2 = 0; a2 < 2 * C; a2++) accr[a2] = cplx{0.0, 0.0};
 
         for (int lev = LEV; lev >= 1; lev--) {
+            asm volatile("" : "+v"(tt));  // per level: the lane's LDS / table addresses are re-derived, not held
             // the level's GGSW values (p, mq) at this thread's two positions (latency hidden by the FFTs)
 #pragma unroll
             for (int p = 0; p < K1; p++)
@@ -264,6 +265,7 @@ __global__ void __launch_bounds__(THREADS, 3)
         WPROF(5);
         s_setprio_c<3>();
         {
+            asm volatile("" : "+v"(tt));
             // this lane's old ACC coefficients from the stash, issued first (their latency hides behind the passes)
             uint64_t old[16];
             if (jvalid) {
