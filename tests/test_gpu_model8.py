@@ -201,6 +201,22 @@ def test_aes8_two_rounds_bit_exact(gpu_context8, oracle_keys8, client8, golden):
     assert np.array_equal(out[0], ref)
 
 
+def test_aes8_eight_blocks_one_round_bit_exact(gpu_context8, oracle_keys8, client8, golden):
+    """Eight blocks in one call: every CBS and extract_bits PBS launch then has 1024 bootstraps, four per CU on 256
+    CUs, the br1024w shape of the bench (64 blocks: 8192 per CBS launch); blocks 0, 3 (a workgroup's fourth
+    ciphertexts) and 7 word for word against the oracle, all eight decrypted against plain AES."""
+    g = golden["test_light"]
+    key = bytes.fromhex(g["key"])
+    ek = b"".join(aes_128.key_schedule_plain(key))
+    rk = client8.encrypt_bits_raw([b for byte in ek for b in aes_128.u8_to_bits(byte)], start_index=70_000)
+    blocks = [bytes([(17 * i + j) & 255 for j in range(16)]) for i in range(8)]
+    cts = client8.encrypt_bits_raw(aes_128.blocks_to_bits(blocks), start_index=75_000).reshape(8, 128, SMALL)
+    out = A8.encrypt_blocks_raw(gpu_context8, rk, cts, rounds=1)
+    assert aes_128.bits_to_blocks(client8.decrypt_bits_raw(out)) == aes_128.expand_key_and_encrypt_blocks(key, blocks, 1)
+    for i in (0, 3, 7):
+        assert np.array_equal(out[i], oracle_keys8.aes8_encrypt_block(rk, cts[i], 1, threads=THREADS)), i
+
+
 def test_aes8_full_fips197_with_fhe_key_schedule(gpu_context8, client8, golden):
     """test_full (test_helper.rs:53-84) for the 8-bit model: FHE key_schedule (fhe_sbox_pbs.rs:123-171)
     then 10 rounds, FIPS-197 C.1, plus a second counter block in the same batch."""
