@@ -9,7 +9,7 @@
 // table (22 KB) fill the LDS, so the accumulator moves out of it:
 //   - the ACC of (ciphertext, polynomial) lives in global memory (a stash [B][k+1][N] u64, L2-resident), read
 //     and written only by the lane that owns the coefficient (j = t + 64 m and j + 512 of the job's wave), so
-//     each lane only reads back its own stores;
+//     each lane only reads back its own stores; the first ciphertext's ACC fits the LDS that is left and stays there;
 //   - after the inverse, the wave also leaves its new ACC in its own LDS job region (u64 [1024]), where the
 //     next step's decomposition reads the rotated coefficients (wave-local, no barrier) before the forward
 //     transform overwrites the region.
@@ -60,7 +60,9 @@ using br1024::wave_sync;
 constexpr int C = 4, CJ = C * K1, THREADS = 64 * CJ;
 static_assert(THREADS == 3 * 256, "one wave per FFT job; the MAC: 256 threads per GGSW column");
 
-inline size_t lds_bytes() { return (size_t)CJ * BUF_STRIDE * 16 + (size_t)lf1k::KERNEL_DOUBLES * 8; }
+// LDS: the 12 job regions, lf1k's table, and the ACC of the workgroup's first ciphertext (its three polynomials
+// stay in LDS; the other three ciphertexts use the global stash)
+inline size_t lds_bytes() { return (size_t)CJ * BUF_STRIDE * 16 + (size_t)lf1k::KERNEL_DOUBLES * 8 + (size_t)K1 * N * 8; }
 
 // lwe_in [B][n+1], lut the test vector GLWE [(k+1) N], bsk the conj(E2)-rescaled Fourier BSK, out [B][k N + 1],
 // acc_g the ACC stash [B][k+1][N]; body_add / out_add as br1024 (homomorphic_shift_boolean); wtab the W_512
@@ -91,6 +93,9 @@ __global__ void __launch_bounds__(THREADS, 3)
     cplx *X = buf + jb * BUF_STRIDE;
     uint64_t *Xu = reinterpret_cast<uint64_t *>(X);
     uint64_t *ag = acc_g + ((size_t)(ct0 + jct) * K1 + jp) * N;  // this job's stash (valid jobs only)
+    // ciphertext 0's ACC lives in LDS after the table (the LDS has room for one of the four): 25% less stash traffic
+    const bool lacc = jct == 0;
+    uint64_t *al = reinterpret_cast<uint64_t *>(s_lf + lf1k::KERNEL_DOUBLES) + jp * N;
 
     for (int i = tid; i < lf1k::KERNEL_DOUBLES; i += THREADS) s_lf[i] = lf[i];
     {  // ACC = X^{-b~} * test vector of this job's polynomial, by the lanes that own the coefficients
@@ -104,7 +109,8 @@ __global__ void __launch_bounds__(THREADS, 3)
             const int j = t + 64 * m;
             const uint64_t v = jvalid ? rotated_coeff(lut + jp * N, j, e0, N) : 0;
             Xu[j] = v;
-            if (jvalid) ag[j] = v;
+            if (lacc) al[j] = v;
+            else if (jvalid) ag[j] = v;
         }
     }
     br512::lds_sync();
@@ -268,7 +274,17 @@ __global__ void __launch_bounds__(THREADS, 3)
             asm volatile("" : "+v"(tt));
             // this lane's old ACC coefficients from the stash, issued first (their latency hides behind the passes)
             uint64_t old[16];
-            if (jvalid) {
+#ifdef TAE_B1KW_NOSTASH  // timing-only bound (garbage results): no ACC-stash loads or stores
+            if (false) {
+#else
+            if (lacc) {
+#pragma unroll
+                for (int m = 0; m < 8; m++) {
+                    old[2 * m] = al[tt + 64 * m];
+                    old[2 * m + 1] = al[tt + 64 * m + M];
+                }
+            } else if (jvalid) {
+#endif
 #pragma unroll
                 for (int m = 0; m < 8; m++) {
                     old[2 * m] = ag[tt + 64 * m];
@@ -317,10 +333,15 @@ __global__ void __launch_bounds__(THREADS, 3)
                 }
                 Xu[j] = a0;
                 Xu[j + M] = a1;
-                if (jvalid) {
+#ifndef TAE_B1KW_NOSTASH
+                if (lacc) {
+                    al[j] = a0;
+                    al[j + M] = a1;
+                } else if (jvalid) {
                     ag[j] = a0;
                     ag[j + M] = a1;
                 }
+#endif
             }
         }
         wave_sync();  // the next decomposition (this wave) reads these LDS ACC writes (in-order LDS)
