@@ -70,10 +70,12 @@ __device__ __forceinline__ void swap32(cplx &x, cplx &y) {
 // 4 x 4 transpose over the lane rows (lanes u, u+16, u+32, u+48) of a DFT16 job: register k of lane
 // row r moves to register r of lane row k
 __device__ __forceinline__ void transpose4(cplx *v) {
+#ifndef TAE_X4_NOSWAP  // timing-only bound (garbage results): no lane transposes
     swap32(v[0], v[2]);
     swap32(v[1], v[3]);
     swap16(v[0], v[1]);
     swap16(v[2], v[3]);
+#endif
 }
 
 __device__ __forceinline__ double lo16(uint32_t w) { return (double)((int32_t)(w << 16) >> 16); }

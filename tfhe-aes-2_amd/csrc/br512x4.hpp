@@ -301,7 +301,12 @@ __global__ void __launch_bounds__(THREADS, 1)
                 const uint64_t x0 = (v0 ^ m0) - (p0 + m0), x1 = (v1 ^ m1) - (p1 + m1);
                 // both halves at once with 16-bit SIMD ops (fft_device.hpp decompose16p)
                 uint32_t dp[LEV];
+#ifdef TAE_X4_NODEC  // timing-only bound (garbage results): bit fields instead of the balanced decomposition
+#pragma unroll
+                for (int l = 0; l < LEV; l++) dp[l] = (uint32_t)(x0 >> (20 * l)) ^ (uint32_t)(x1 >> (20 * l + 8));
+#else
                 decompose16p<LEV, BLOG>(x0, x1, dp);
+#endif
                 if constexpr (DBYTES) {
 #pragma unroll
                     for (int l = 0; l < LEV; l += 2) {  // bytes 0, 1: level l (j, j + M); bytes 2, 3: level l + 1
@@ -476,12 +481,16 @@ __global__ void __launch_bounds__(THREADS, 1)
                 for (int k2 = 0; k2 < 4; k2++) {
                     const int j = ll + 64 * k2;  // m = r + 4 k2 -> j = u + 16 m
                     const cplx t = cmul(v[k2], s_untw[j]);  // x 2^-8 (exact) in the conversion
+#ifdef TAE_X4_NOTORUS  // timing-only bound (garbage results): the f64 bit patterns added instead of the conversion
+                    uint64_t a0 = poly[j] + f64_bits(t.re), a1 = poly[j + M] + f64_bits(t.im);
+#else
                     bool o0, o1;
                     uint64_t a0 = torus_add_fast_sh<8>(t.re, poly[j], o0), a1 = torus_add_fast_sh<8>(t.im, poly[j + M], o1);
                     if (__builtin_amdgcn_ballot_w64(!(o0 && o1))) {  // zeros, out-of-range magnitudes (rare)
                         a0 = poly[j] + from_torus_bits(t.re * 0x1p-8);
                         a1 = poly[j + M] + from_torus_bits(t.im * 0x1p-8);
                     }
+#endif
                     poly[j] = a0;
                     poly[j + M] = a1;
                 }
