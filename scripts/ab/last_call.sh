@@ -1,3 +1,3 @@
 set -o pipefail
 cd /root/repo
-PASSES=2 VARIANTS="base:: noswap:noswap.so: nodec:nodec.so: notorus:notorus.so: all3:all3.so:" CLOCK=1 bash scripts/ab/ab.sh pbs1 > gpurun_out/ab_x4_bounds.txt 2>&1
+timeout -k 10 500 python -u scripts/probes/stage_overlap.py 224 236 240 > gpurun_out/overlap2.txt 2>&1

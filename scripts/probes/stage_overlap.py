@@ -38,9 +38,13 @@ def context(mask):
     else:
         os.environ.pop("TAE_CU_MASK", None)
     try:
-        return tfhe_aes.context_from_raw(pid, keys, device=0)
+        ctx = tfhe_aes.context_from_raw(pid, keys, device=0)
     finally:
         os.environ.pop("TAE_CU_MASK", None)
+    # a caller stream of its own: the device-memory stage entry points then order after an event on that
+    # stream instead of hipDeviceSynchronize (which would serialise the two contexts' launches)
+    ctx.set_caller_stream(torch.cuda.Stream())
+    return ctx
 
 
 def pbs(ctx):
