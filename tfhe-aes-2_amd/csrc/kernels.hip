@@ -702,15 +702,17 @@ void Engine::init_common() {
         HIPC(hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, device_));
         const bool hi = !strncmp(cm, "hi:", 3);
         if (!hi && strncmp(cm, "lo:", 3)) throw std::runtime_error("TAE_CU_MASK must be lo:N or hi:N");
-        const int nc = atoi(cm + 3);
-        if (nc < 1 || nc > total || total > 256) throw std::runtime_error("TAE_CU_MASK: bad CU count");
+        char *end = nullptr;
+        const long nc = strtol(cm + 3, &end, 10);
+        if (end == cm + 3 || *end || nc < 1 || nc > total || total > 256)
+            throw std::runtime_error(std::string("TAE_CU_MASK: bad CU count in '") + cm + "'");
         uint32_t mask[8] = {0};
         for (int c = 0; c < nc; c++) {
             const int b = hi ? total - 1 - c : c;
             mask[b >> 5] |= 1u << (b & 31);
         }
         HIPC(hipExtStreamCreateWithCUMask(&stream_, 8, mask));
-        mask_cus = nc;
+        mask_cus = (int)nc;
     } else {
         HIPC(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     }
